@@ -1,0 +1,39 @@
+# Build libcairo_amd.so (HIP for gfx950 + host C++) and the test oracle.
+# `python -c "import __graft_entry__ as g; g.build()"` runs this.
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     = g++
+ARCH    ?= gfx950
+CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+HIPFLAGS = --offload-arch=$(ARCH) $(CXXFLAGS) -munsafe-fp-atomics
+SRC      = cairo_amd/csrc
+OBJ      = build/obj
+LIB      = cairo_amd/_lib/libcairo_amd.so
+ORACLE   = oracle/liboracle.so
+
+HIP_SRCS = $(SRC)/kernels.hip $(SRC)/backend.hip
+CPP_SRCS = $(SRC)/entropy.cpp $(SRC)/bitstream.cpp $(SRC)/encoder.cpp $(SRC)/decoder.cpp
+OBJS     = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
+HDRS     = $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
+
+all: $(LIB) $(ORACLE)
+
+$(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(dir $(LIB))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+
+# Test infrastructure only (tests/, smoke(), bench.py cpu_baseline).
+$(ORACLE): oracle/evx_oracle.c oracle/evx_oracle.h
+	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ oracle/evx_oracle.c -lm
+
+clean:
+	rm -rf build $(LIB) $(ORACLE)
+
+.PHONY: all clean

@@ -1,0 +1,340 @@
+"""cairo_amd -- MI355X-native EVX-1 (hinike/cairo) encode path.
+
+The product is ``_lib/libcairo_amd.so``: hand-written HIP kernels for gfx950
+(convert, inter search, macroblock wavefront, deblock), the host entropy stage
+and the drop-in ``evx1_encoder`` / ``bit_stream`` C++ API.  This module is a
+thin ctypes view of its C ABI (``include/cairo_amd.h``) for tests, the bench
+and Python callers.  There is no Python or CPU fallback for the hot path: if
+the library is missing, importing the bindings raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libcairo_amd.so")
+
+# evx_block_desc (reference common.h:78-95, pack(2), 16 bytes)
+BLOCK_DESC = np.dtype(
+    [
+        ("block_type", "<u4"),
+        ("prediction_target", "u1"),
+        ("pad", "u1"),
+        ("motion_x", "<i2"),
+        ("motion_y", "<i2"),
+        ("sp_pred", "u1"),
+        ("sp_amount", "u1"),
+        ("sp_index", "u1"),
+        ("q_index", "u1"),
+        ("variance", "<i2"),
+    ]
+)
+assert BLOCK_DESC.itemsize == 16
+
+EVX_SUCCESS = 0
+EVX_ERROR_HARDWAREFAIL = 5
+
+
+class CairoError(RuntimeError):
+    def __init__(self, what: str, status: int):
+        super().__init__(f"{what} failed with evx_status {status}")
+        self.status = status
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libcairo_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build()"
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, U, V = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, None
+    sig = {
+        "cairo_ctx_create": (I, [U, U, U, I, ctypes.POINTER(P)]),
+        "cairo_ctx_destroy": (I, [P]),
+        "cairo_ctx_reset": (I, [P]),
+        "cairo_ctx_submit": (I, [P, P, I, U, U, U, ctypes.POINTER(I)]),
+        "cairo_ctx_wait": (I, [P, I, P]),
+        "cairo_ctx_release": (I, [P, I]),
+        "cairo_ctx_sync": (I, [P]),
+        "cairo_ctx_stages": (I, [P]),
+        "cairo_ctx_read_planes": (I, [P, I, P, P, P]),
+        "cairo_ctx_read_inter": (I, [P, P, P]),
+        "cairo_ctx_read_table": (I, [P, P]),
+        "cairo_ctx_set_debug": (I, [P, I]),
+        "cairo_ctx_read_predeblock": (I, [P, P, P, P]),
+        "cairo_ctx_set_profiling": (I, [P, I]),
+        "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
+        "cairo_ctx_set_workgroups": (I, [P, I, I]),
+        "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
+        "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
+        "evx_encoder_create": (I, [ctypes.POINTER(P)]),
+        "evx_encoder_destroy": (I, [P]),
+        "evx_encoder_clear": (I, [P]),
+        "evx_encoder_insert_intra": (I, [P]),
+        "evx_encoder_set_quality": (I, [P, ctypes.c_uint8]),
+        "evx_encoder_encode": (I, [P, P, U, U, P]),
+        "evx_encoder_set_ring": (I, [P, U]),
+        "evx_encoder_set_device": (I, [P, I]),
+        "evx_bitstream_create": (P, [U]),
+        "evx_bitstream_destroy": (V, [P]),
+        "evx_bitstream_data": (P, [P]),
+        "evx_bitstream_occupancy": (U, [P]),
+        "evx_bitstream_empty": (V, [P]),
+        "cairo_make_band4": (V, [P, U, U, U, U]),
+        "cairo_version": (ctypes.c_char_p, []),
+        "cairo_device_count": (I, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _ck(status: int, what: str) -> None:
+    if status != EVX_SUCCESS:
+        raise CairoError(what, status)
+
+
+def _ptr(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def make_band4(w: int, h: int, t: int, seed: int = 1234) -> np.ndarray:
+    """band4 synthetic RGB888 frame, shape (h, w, 3)."""
+    out = np.empty((h, w, 3), np.uint8)
+    lib().cairo_make_band4(_ptr(out), w, h, t, seed)
+    return out
+
+
+class _FrameResult(ctypes.Structure):
+    _fields_ = [
+        ("block_table", ctypes.c_void_p),
+        ("coef_y", ctypes.c_void_p),
+        ("coef_u", ctypes.c_void_p),
+        ("coef_v", ctypes.c_void_p),
+        ("wa", ctypes.c_uint32),
+        ("ha", ctypes.c_uint32),
+        ("wmb", ctypes.c_uint32),
+        ("hmb", ctypes.c_uint32),
+        ("index", ctypes.c_uint32),
+        ("type", ctypes.c_uint32),
+        ("quality", ctypes.c_uint32),
+    ]
+
+
+@dataclass
+class FrameOutputs:
+    """Host copies of one frame's outputs (block table + output_cache)."""
+
+    table: np.ndarray  # (mbs,) BLOCK_DESC
+    coef_y: np.ndarray
+    coef_u: np.ndarray
+    coef_v: np.ndarray
+
+
+def _view(addr: int, dtype, count: int) -> np.ndarray:
+    buf = (ctypes.c_char * (count * np.dtype(dtype).itemsize)).from_address(addr)
+    return np.frombuffer(buf, dtype=dtype, count=count)
+
+
+class Context:
+    """The encode-path backend (``cairo_ctx_*``): one encoder's device state."""
+
+    def __init__(self, width: int, height: int, ring: int = 4, device: int = 0):
+        self.L = lib()
+        self.width, self.height, self.ring, self.device = width, height, ring, device
+        self.wa, self.ha = (width + 15) & ~15, (height + 15) & ~15
+        self.wmb, self.hmb = self.wa // 16, self.ha // 16
+        p = ctypes.c_void_p()
+        _ck(self.L.cairo_ctx_create(width, height, ring, device, ctypes.byref(p)), "cairo_ctx_create")
+        self.h = p
+
+    def close(self) -> None:
+        if self.h:
+            self.L.cairo_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> int:
+        t = ctypes.c_int()
+        ptr = rgb if on_device else _ptr(rgb)
+        _ck(
+            self.L.cairo_ctx_submit(self.h, ptr, int(on_device), index, int(inter), quality, ctypes.byref(t)),
+            "cairo_ctx_submit",
+        )
+        return t.value
+
+    def wait(self, ticket: int, copy: bool = True) -> FrameOutputs:
+        r = _FrameResult()
+        _ck(self.L.cairo_ctx_wait(self.h, ticket, ctypes.byref(r)), "cairo_ctx_wait")
+        ny, nc = r.wa * r.ha, (r.wa // 2) * (r.ha // 2)
+        mbs = r.wmb * r.hmb
+        out = FrameOutputs(
+            _view(r.block_table, BLOCK_DESC, mbs),
+            _view(r.coef_y, np.int16, ny).reshape(r.ha, r.wa),
+            _view(r.coef_u, np.int16, nc).reshape(r.ha // 2, r.wa // 2),
+            _view(r.coef_v, np.int16, nc).reshape(r.ha // 2, r.wa // 2),
+        )
+        if copy:
+            out = FrameOutputs(*(a.copy() for a in (out.table, out.coef_y, out.coef_u, out.coef_v)))
+        return out
+
+    def release(self, ticket: int) -> None:
+        _ck(self.L.cairo_ctx_release(self.h, ticket), "cairo_ctx_release")
+
+    def encode_frame(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> FrameOutputs:
+        t = self.submit(rgb, index, inter, quality, on_device)
+        try:
+            return self.wait(t, copy=True)
+        finally:
+            self.release(t)
+
+    def sync(self) -> None:
+        _ck(self.L.cairo_ctx_sync(self.h), "cairo_ctx_sync")
+
+    def read_planes(self, which: int):
+        """which: 0 input, 1 output_cache, 2+k ring slot k -> (y, u, v)."""
+        y = np.empty((self.ha, self.wa), np.int16)
+        u = np.empty((self.ha // 2, self.wa // 2), np.int16)
+        v = np.empty_like(u)
+        _ck(self.L.cairo_ctx_read_planes(self.h, which, _ptr(y), _ptr(u), _ptr(v)), "read_planes")
+        return y, u, v
+
+    def read_inter(self):
+        n = self.wmb * self.hmb * max(self.ring - 1, 0)
+        d = np.zeros(n, BLOCK_DESC)
+        s = np.zeros(n, np.int32)
+        if n:
+            _ck(self.L.cairo_ctx_read_inter(self.h, _ptr(d), _ptr(s)), "read_inter")
+        return d, s
+
+    def read_table(self):
+        t = np.zeros(self.wmb * self.hmb, BLOCK_DESC)
+        _ck(self.L.cairo_ctx_read_table(self.h, _ptr(t)), "read_table")
+        return t
+
+    def set_debug(self, flags: int) -> None:
+        _ck(self.L.cairo_ctx_set_debug(self.h, flags), "set_debug")
+
+    def read_predeblock(self):
+        y = np.empty((self.ha, self.wa), np.int16)
+        u = np.empty((self.ha // 2, self.wa // 2), np.int16)
+        v = np.empty_like(u)
+        _ck(self.L.cairo_ctx_read_predeblock(self.h, _ptr(y), _ptr(u), _ptr(v)), "read_predeblock")
+        return y, u, v
+
+    def set_profiling(self, enable: bool) -> None:
+        _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")
+
+    def take_timings(self):
+        ms = (ctypes.c_double * 4)()
+        n = ctypes.c_int()
+        _ck(self.L.cairo_ctx_take_timings(self.h, ms, ctypes.byref(n)), "take_timings")
+        return list(ms), n.value
+
+    def set_workgroups(self, rows: int = 0, deblock: int = 0) -> None:
+        _ck(self.L.cairo_ctx_set_workgroups(self.h, rows, deblock), "set_workgroups")
+
+
+def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):
+    """Host entropy stage on explicit inputs -> (bytes, nbits)."""
+    cap = capacity_bytes or (cy.size * 8 + 65536)
+    out = np.zeros(cap, np.uint8)
+    pos = ctypes.c_uint32(0)
+    t = np.ascontiguousarray(table).view(np.uint8)
+    cy, cu, cv = (np.ascontiguousarray(a, dtype=np.int16) for a in (cy, cu, cv))
+    _ck(
+        lib().cairo_serialize_slice(_ptr(t), wmb, hmb, ring, _ptr(cy), _ptr(cu), _ptr(cv), _ptr(out), cap, ctypes.byref(pos)),
+        "cairo_serialize_slice",
+    )
+    n = pos.value
+    return out[: (n + 7) // 8].tobytes(), n
+
+
+class BitStream:
+    """evx::bit_stream owned from Python."""
+
+    def __init__(self, size_bits: int):
+        self.L = lib()
+        self.h = self.L.evx_bitstream_create(size_bits)
+        if not self.h:
+            raise MemoryError("evx_bitstream_create")
+
+    def bits(self) -> int:
+        return self.L.evx_bitstream_occupancy(self.h)
+
+    def data(self) -> bytes:
+        n = (self.bits() + 7) // 8
+        return ctypes.string_at(self.L.evx_bitstream_data(self.h), n) if n else b""
+
+    def empty(self) -> None:
+        self.L.evx_bitstream_empty(self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.evx_bitstream_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Encoder:
+    """The drop-in evx1_encoder (reference evx1.h:66-94) through its C view."""
+
+    def __init__(self, ring: int = 4, device: int = 0):
+        self.L = lib()
+        p = ctypes.c_void_p()
+        _ck(self.L.evx_encoder_create(ctypes.byref(p)), "create_encoder")
+        self.h = p
+        if ring != 4:
+            _ck(self.L.evx_encoder_set_ring(self.h, ring), "set_ring")
+        if device:
+            _ck(self.L.evx_encoder_set_device(self.h, device), "set_device")
+
+    def set_quality(self, q: int) -> None:
+        _ck(self.L.evx_encoder_set_quality(self.h, q), "set_quality")
+
+    def insert_intra(self) -> None:
+        _ck(self.L.evx_encoder_insert_intra(self.h), "insert_intra")
+
+    def clear(self) -> None:
+        _ck(self.L.evx_encoder_clear(self.h), "clear")
+
+    def encode(self, rgb: np.ndarray, bs: BitStream) -> None:
+        h, w = rgb.shape[:2]
+        _ck(self.L.evx_encoder_encode(self.h, _ptr(np.ascontiguousarray(rgb)), w, h, bs.h), "encode")
+
+    def close(self) -> None:
+        if self.h:
+            self.L.evx_encoder_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    return lib().cairo_device_count()

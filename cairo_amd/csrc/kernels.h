@@ -1,0 +1,70 @@
+// cairo_amd/csrc/kernels.h -- launch interface of the gfx950 encode-path kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "evx_defs.h"
+
+namespace cairo {
+
+// One plane set in HBM: int16 planes, pitch == plane width (image.cpp:55-68).
+struct PlaneSet {
+  int16_t* y;
+  int16_t* u;
+  int16_t* v;
+};
+
+// Plane set of ring slot k inside one contiguous allocation.
+__host__ __device__ inline PlaneSet ring_slot(int16_t* base, size_t slot_elems, int wa, int ha,
+                                              int k) {
+  PlaneSet p;
+  p.y = base + (size_t)k * slot_elems;
+  p.u = p.y + (size_t)wa * ha;
+  p.v = p.u + (size_t)(wa / 2) * (ha / 2);
+  return p;
+}
+
+// Per-frame kernel arguments (passed by value).
+struct FrameArgs {
+  int wa, ha;          // frame size aligned to 16 (evx1enc.cpp:79-80)
+  int w, h;            // nominal frame size (RGB input)
+  int wmb, hmb;        // macroblocks per row / column
+  int ring;            // R = ring size (EVX_REFERENCE_FRAME_COUNT)
+  int index;           // frame index (common.cpp:192-195 ring addressing)
+  int inter;           // frame type: 0 intra, 1 inter
+  int quality;         // frame quality 1..31
+  const uint8_t* rgb;  // RGB888, pitch 3*w
+  PlaneSet in;         // input_cache
+  PlaneSet coef;       // output_cache (quantized coefficients, persistent)
+  int16_t* ring_base;       // R contiguous plane sets (Y, U, V each), slot k at
+  size_t slot_elems;        //   ring_base + k * slot_elems
+  BlockDesc* table;        // block table [wmb*hmb]
+  BlockDesc* inter_desc;   // [(off-1)*mbs + mb]
+  int32_t* inter_sad;      // [(off-1)*mbs + mb]
+  int32_t* sync;           // SyncLayout words, zeroed before every frame
+};
+
+// Words of FrameArgs::sync (all int32, zeroed per frame).
+struct SyncLayout {
+  static constexpr int kErr = 0;         // nonzero: a bounded wait timed out
+  static constexpr int kRowTicket = 1;   // K2 row dequeue
+  static constexpr int kDbTicket = 2;    // K3 band dequeue, 3 planes
+  static constexpr int kRowDone = 8;     // K2 per-row progress [hmb]
+  // K3 per-band progress for plane p at kRowDone + hmb + p * max_bands
+  __host__ __device__ static int words(int hmb) { return kRowDone + hmb + 3 * (2 * hmb + 2) + 8; }
+  __host__ __device__ static int db_base(int hmb, int plane) { return kRowDone + hmb + plane * (2 * hmb + 2); }
+};
+
+hipError_t launch_convert(const FrameArgs& a, hipStream_t s);
+hipError_t launch_inter_search(const FrameArgs& a, hipStream_t s);
+hipError_t launch_mb_rows(const FrameArgs& a, int workgroups, hipStream_t s);
+hipError_t launch_deblock(const FrameArgs& a, int workgroups, hipStream_t s);
+
+// Known-answer entry points: apply the device transform / quantizer code to
+// a batch of macroblocks (6 blocks of 64 int16 each, block-major).
+hipError_t launch_kat_transform(const int16_t* src, const int16_t* pred, int16_t* coef,
+                                int16_t* recon, const uint8_t* qtype, int32_t* qvar,
+                                int count, hipStream_t s);
+
+}  // namespace cairo

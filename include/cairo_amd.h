@@ -1,0 +1,133 @@
+/*
+ * include/cairo_amd.h -- C ABI of libcairo_amd.so, the MI355X-native EVX-1
+ * encode path.  Plain pointers and sizes only.
+ *
+ * Two layers:
+ *
+ *  1. The encode-path backend ("cairo_ctx_*").  It replaces the hot stages
+ *     inside engine_encode_frame (reference encode.cpp:205-232): convert_image
+ *     (convert.cpp:95-160), encode_slice (encode.cpp:165-203, with
+ *     motion.cpp / transform.cpp / quantize.cpp / decode.cpp:15-144) and
+ *     deblock_image_filter (deblock.cpp:277-284).  Its outputs are exactly what
+ *     the host entropy stage serialize_slice (serialize.cpp:319-340) consumes:
+ *     the block table (evx_block_desc[], common.h:78-95, 16 B each) and the
+ *     persistent quantized-coefficient planes (output_cache, common.h:108).
+ *
+ *  2. C wrappers of the drop-in C++ API (include/evx1.h), for FFI callers
+ *     (ctypes): evx_encoder_* mirror evx1_encoder (reference evx1.h:66-94) and
+ *     create_encoder / destroy_encoder (evx1.cpp:8-63); cairo_serialize_slice
+ *     exposes the host entropy stage on its own.
+ *
+ * Status codes are evx_status values (reference base.h:150-172); a HIP
+ * failure or a timed-out in-kernel wait maps to EVX_ERROR_HARDWAREFAIL (5).
+ */
+#ifndef CAIRO_AMD_H
+#define CAIRO_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAIRO_API __attribute__((visibility("default")))
+
+typedef struct cairo_ctx cairo_ctx;
+
+/* Host-visible outputs of one frame; valid until cairo_ctx_release(ticket). */
+typedef struct cairo_frame_result {
+  const uint8_t *block_table; /* wmb*hmb evx_block_desc (16 B, pack(2) layout) */
+  const int16_t *coef_y;      /* output_cache Y, wa x ha, pitch wa            */
+  const int16_t *coef_u;      /* output_cache U, wa/2 x ha/2, pitch wa/2      */
+  const int16_t *coef_v;      /* output_cache V                               */
+  uint32_t wa, ha, wmb, hmb;
+  uint32_t index, type, quality;
+} cairo_frame_result;
+
+/* Context = one encoder's device state: R ring slots, input and output_cache
+ * planes, block table, inter-search records, staging.  width/height are the
+ * nominal frame size (aligned up to 16 internally, evx1enc.cpp:79-80); ring is
+ * R = EVX_REFERENCE_FRAME_COUNT (2..8); device is the HIP ordinal. */
+CAIRO_API int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
+                               cairo_ctx **out);
+CAIRO_API int cairo_ctx_destroy(cairo_ctx *ctx);
+/* Zero every plane (fresh-encoder state, common.cpp:79-150). */
+CAIRO_API int cairo_ctx_reset(cairo_ctx *ctx);
+
+/* Enqueue the hot path for frame (index, type 0=intra/1=inter, quality).
+ * rgb is RGB888 with pitch 3*width, in host memory (rgb_on_device = 0) or
+ * device memory of this context's GPU (1).  Returns a ticket. */
+CAIRO_API int cairo_ctx_submit(cairo_ctx *ctx, const uint8_t *rgb, int rgb_on_device,
+                               uint32_t index, uint32_t type, uint32_t quality, int *ticket);
+/* Wait until the frame's block table and coefficients are host-visible. */
+CAIRO_API int cairo_ctx_wait(cairo_ctx *ctx, int ticket, cairo_frame_result *out);
+/* Hand the ticket's staging buffers back (required before ticket+stages). */
+CAIRO_API int cairo_ctx_release(cairo_ctx *ctx, int ticket);
+/* Block until all submitted GPU work (including the deblock) is finished. */
+CAIRO_API int cairo_ctx_sync(cairo_ctx *ctx);
+CAIRO_API int cairo_ctx_stages(const cairo_ctx *ctx);
+
+/* Introspection (synchronous).  which: 0 input, 1 output_cache, 2+k slot k. */
+CAIRO_API int cairo_ctx_read_planes(cairo_ctx *ctx, int which, int16_t *y, int16_t *u,
+                                    int16_t *v);
+/* Inter-search records of the last frame: (ring-1)*mbs descs and SADs. */
+CAIRO_API int cairo_ctx_read_inter(cairo_ctx *ctx, uint8_t *descs, int32_t *sads);
+CAIRO_API int cairo_ctx_read_table(cairo_ctx *ctx, uint8_t *table);
+/* Debug: flags & 1 snapshots the reconstruction before the deblock of every
+ * frame; cairo_ctx_read_predeblock returns the last snapshot. */
+CAIRO_API int cairo_ctx_set_debug(cairo_ctx *ctx, int flags);
+CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, int16_t *v);
+
+/* Per-kernel timing (HIP events on the kernels' stream), opt-in. */
+CAIRO_API int cairo_ctx_set_profiling(cairo_ctx *ctx, int enable);
+/* Accumulated ms per kernel since the last call: [convert, inter, mb_rows,
+ * deblock], and the number of frames they cover; resets the accumulators. */
+CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[4], int *frames);
+/* Workgroup counts of the wavefront kernels (0 = default). */
+CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows, int deblock);
+
+/* Known-answer check of the device transform chain: count macroblocks of 384
+ * int16 (block-major: Y TL,TR,BL,BR, U, V; 64 each).  qtype[2m] = block type,
+ * qtype[2m+1] = frame quality.  Host buffers in and out. */
+CAIRO_API int cairo_kat_transform(const int16_t *src, const int16_t *pred, const uint8_t *qtype,
+                                  int count, int16_t *coef, int16_t *recon, int32_t *qvar,
+                                  int device);
+
+/* ---- host entropy stage (serialize_slice, serialize.cpp:319-340) ---------
+ * Appends the ABAC payload of one frame to out (LSB-first bit order) at bit
+ * *bit_pos, advancing it.  coef planes have pitch wa (luma) / wa/2 (chroma). */
+CAIRO_API int cairo_serialize_slice(const uint8_t *block_table, uint32_t wmb, uint32_t hmb,
+                                    uint32_t ring, const int16_t *coef_y, const int16_t *coef_u,
+                                    const int16_t *coef_v, uint8_t *out, uint32_t out_bytes,
+                                    uint32_t *bit_pos);
+
+/* ---- drop-in encoder, C view of evx1_encoder (evx1.h:66-94) ------------- */
+CAIRO_API int evx_encoder_create(void **enc);
+CAIRO_API int evx_encoder_destroy(void *enc);
+CAIRO_API int evx_encoder_clear(void *enc);
+CAIRO_API int evx_encoder_insert_intra(void *enc);
+CAIRO_API int evx_encoder_set_quality(void *enc, uint8_t quality);
+/* Encode one RGB888 frame, appending to the bit stream bs (evx_bitstream_*). */
+CAIRO_API int evx_encoder_encode(void *enc, const void *rgb, uint32_t width, uint32_t height,
+                                 void *bs);
+CAIRO_API int evx_encoder_set_ring(void *enc, uint32_t ring); /* before first encode */
+CAIRO_API int evx_encoder_set_device(void *enc, int device);  /* before first encode */
+
+/* bit_stream (reference bitstream.h:43-92) */
+CAIRO_API void *evx_bitstream_create(uint32_t size_in_bits);
+CAIRO_API void evx_bitstream_destroy(void *bs);
+CAIRO_API const uint8_t *evx_bitstream_data(void *bs);
+CAIRO_API uint32_t evx_bitstream_occupancy(void *bs); /* bits */
+CAIRO_API void evx_bitstream_empty(void *bs);
+
+/* band4 synthetic content generator; RGB888, pitch 3*w. */
+CAIRO_API void cairo_make_band4(uint8_t *rgb, uint32_t w, uint32_t h, uint32_t t, uint32_t seed);
+
+/* Library/device information. */
+CAIRO_API const char *cairo_version(void);
+CAIRO_API int cairo_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

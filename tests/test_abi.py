@@ -1,0 +1,52 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares
+(no compute calls: this runs without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_c_symbols():
+    text = open(os.path.join(ROOT, "include", "cairo_amd.h")).read()
+    return sorted(set(re.findall(r"CAIRO_API\s+[\w\s\*]+?\b((?:cairo|evx)_\w+)\s*\(", text)))
+
+
+def test_library_exports_c_abi(cairo):
+    names = _declared_c_symbols()
+    assert len(names) >= 30
+    L = cairo.lib()
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_library_exports_cpp_api(cairo):
+    out = subprocess.run(["nm", "-D", "--defined-only", cairo.LIB_PATH], capture_output=True, text=True).stdout
+    # evx1.cpp:8-63 free functions, mangled as in the reference
+    for sym in ["_ZN3evx14create_encoderEPPNS_12evx1_encoderE", "_ZN3evx15destroy_encoderEPNS_12evx1_encoderE",
+                "_ZN3evx14create_decoderEPPNS_12evx1_decoderE", "_ZN3evx15destroy_decoderEPNS_12evx1_decoderE",
+                "_ZN3evx10bit_streamC1Ej", "_ZN3evx10bit_stream10write_bitsEPvj"]:
+        assert sym in out, sym
+
+
+def test_library_carries_gfx950_code(cairo):
+    data = open(cairo.LIB_PATH, "rb").read()
+    assert b"__CLANG_OFFLOAD_BUNDLE__" in data and b"gfx950" in data
+
+
+def test_bitstream_semantics(cairo):
+    L = cairo.lib()
+    bs = cairo.BitStream(64)
+    L_ = bs.L
+    # write_bits via the encoder path is exercised on GPU; here: capacity + empty()
+    assert bs.bits() == 0
+    bs.empty()
+    assert bs.data() == b""
+
+
+def test_band4_product_generator_matches_oracle(orc, cairo):
+    for t in (0, 3):
+        assert np.array_equal(cairo.make_band4(96, 64, t), orc.make_frame(96, 64, t))

@@ -1,0 +1,198 @@
+"""GPU parity: the HIP encode path (libcairo_amd.so) against the oracle.
+
+Bit-exact on every intermediate the reference exposes: the transform /
+quantize / reconstruct chain on random macroblocks (KAT), and per frame the
+inter-search records, the block table, the quantized coefficients
+(output_cache), the reconstruction before and after the deblocking filter,
+and finally whole streams through the drop-in evx1_encoder API against the
+frozen stream hashes in tests/golden/oracle_streams.json (themselves pinned
+to the reference's recorded sizes, tests/test_oracle.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# ---------------------------------------------------------------------------
+# KAT: transform -> VAQ -> quantize -> dequantize -> inverse transform (+pred)
+# ---------------------------------------------------------------------------
+
+def _luma16(blocks):
+    """block-major (6, 8, 8) -> 16x16 luma of quadrants TL TR BL BR."""
+    y = np.empty((16, 16), np.int16)
+    for b in range(4):
+        y[(b >> 1) * 8:(b >> 1) * 8 + 8, (b & 1) * 8:(b & 1) * 8 + 8] = blocks[b]
+    return y
+
+
+def _blocks(y16, u, v):
+    out = np.empty((6, 8, 8), np.int16)
+    for b in range(4):
+        out[b] = y16[(b >> 1) * 8:(b >> 1) * 8 + 8, (b & 1) * 8:(b & 1) * 8 + 8]
+    out[4], out[5] = u, v
+    return out
+
+
+def _oracle_chain(orc, src, pred, typ, quality):
+    L = orc.lib()
+    P = lambda a: a.ctypes.data  # noqa: E731
+    coef = np.zeros((6, 8, 8), np.int16)
+    for b in range(6):
+        s = np.ascontiguousarray(src[b])
+        if typ == 1:
+            L.orc_transform_8x8(P(s), 8, P(coef[b]), 8)
+        else:
+            p = np.ascontiguousarray(pred[b])
+            L.orc_sub_transform_8x8(P(s), 8, P(p), 8, P(coef[b]), 8)
+    y16 = _luma16(coef)
+    q = L.orc_vaq(quality, P(y16), 16)
+    var = L.orc_variance2(P(y16), 16)
+    qy, qu, qv = np.zeros((16, 16), np.int16), np.zeros((8, 8), np.int16), np.zeros((8, 8), np.int16)
+    u, v = np.ascontiguousarray(coef[4]), np.ascontiguousarray(coef[5])
+    L.orc_quantize_mb(q, typ, P(y16), P(u), P(v), P(qy), P(qu), P(qv))
+    dy, du, dv = np.zeros_like(qy), np.zeros_like(qu), np.zeros_like(qv)
+    L.orc_dequantize_mb(q, typ, P(qy), P(qu), P(qv), P(dy), P(du), P(dv))
+    deq = _blocks(dy, du, dv)
+    rec = np.zeros((6, 8, 8), np.int16)
+    for b in range(6):
+        d = np.ascontiguousarray(deq[b])
+        if typ == 1:
+            L.orc_inverse_transform_8x8(P(d), 8, P(rec[b]), 8)
+        else:
+            p = np.ascontiguousarray(pred[b])
+            L.orc_inverse_transform_add_8x8(P(d), 8, P(p), 8, P(rec[b]), 8)
+    return _blocks(qy, qu, qv), rec, q, var
+
+
+def test_kat_transform_chain(orc, cairo):
+    rng = np.random.default_rng(2024)
+    n = 96
+    src = rng.integers(16, 272, (n, 6, 8, 8)).astype(np.int16)
+    pred = rng.integers(-200, 600, (n, 6, 8, 8)).astype(np.int16)
+    # edge content: flat, extreme, checkerboard
+    src[0] = 16
+    src[1] = 271
+    pred[2] = -32000
+    src[3] = np.where((np.indices((6, 8, 8)).sum(0) % 2) == 0, 16, 271)
+    types = np.array([1, 0, 2, 3] * (n // 4), np.uint8)
+    quals = np.array([1, 4, 8, 16, 24, 31] * (n // 6), np.uint8)
+    qtype = np.stack([types, quals], 1).astype(np.uint8).copy()
+    coef = np.zeros((n, 6, 8, 8), np.int16)
+    rec = np.zeros_like(coef)
+    qv = np.zeros((n, 2), np.int32)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    st = cairo.lib().cairo_kat_transform(P(src), P(pred), P(qtype), n, P(coef), P(rec), P(qv), 0)
+    assert st == 0
+    for m in range(n):
+        c, r, q, var = _oracle_chain(orc, src[m], pred[m], int(types[m]), int(quals[m]))
+        assert qv[m, 0] == q, m
+        assert qv[m, 1] == var, m
+        np.testing.assert_array_equal(coef[m], c, err_msg=f"coef mb {m}")
+        np.testing.assert_array_equal(rec[m], r, err_msg=f"recon mb {m}")
+
+
+# ---------------------------------------------------------------------------
+# Frame-level parity
+# ---------------------------------------------------------------------------
+
+def _table_equal(a, b, what):
+    for f in a.dtype.names:
+        if f == "pad":
+            continue
+        bad = np.nonzero(a[f] != b[f])[0]
+        assert bad.size == 0, f"{what}: field {f} differs at MBs {bad[:10]} gpu={a[f][bad[:5]]} ref={b[f][bad[:5]]}"
+
+
+def _run_frames(orc, cairo, w, h, ring, q, frames, intra_only=False, check_inter=True):
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    ctx = cairo.Context(w, h, ring)
+    ctx.set_debug(1)
+    for t in range(frames):
+        rgb = orc.make_frame(w, h, t)
+        inter = t > 0 and not intra_only
+        if intra_only:
+            e.insert_intra()
+        e.encode(rgb)
+        out = ctx.encode_frame(rgb, t, inter, q)
+        tag = f"{w}x{h} R={ring} q={q} frame {t}"
+        gy, gu, gv = ctx.read_planes(0)
+        oy, ou, ov = e.planes(0)
+        np.testing.assert_array_equal(gy, oy, err_msg=f"{tag}: input Y")
+        np.testing.assert_array_equal(gu, ou, err_msg=f"{tag}: input U")
+        if inter and check_inter and ring > 1:
+            gd, gs = ctx.read_inter()
+            od, os_ = e.inter_records()
+            _table_equal(gd, od, f"{tag}: inter records")
+            np.testing.assert_array_equal(gs, os_, err_msg=f"{tag}: inter SAD")
+        _table_equal(out.table, e.block_table(), f"{tag}: block table")
+        oy, ou, ov = e.planes(1)
+        np.testing.assert_array_equal(out.coef_y, oy, err_msg=f"{tag}: coef Y")
+        np.testing.assert_array_equal(out.coef_u, ou, err_msg=f"{tag}: coef U")
+        np.testing.assert_array_equal(out.coef_v, ov, err_msg=f"{tag}: coef V")
+        py, pu, pv = ctx.read_predeblock()
+        ry, ru, rv = e.predeblock()
+        np.testing.assert_array_equal(py, ry, err_msg=f"{tag}: recon Y (pre-deblock)")
+        np.testing.assert_array_equal(pu, ru, err_msg=f"{tag}: recon U (pre-deblock)")
+        np.testing.assert_array_equal(pv, rv, err_msg=f"{tag}: recon V (pre-deblock)")
+        slot = 2 + t % ring
+        gy, gu, gv = ctx.read_planes(slot)
+        oy, ou, ov = e.planes(slot)
+        np.testing.assert_array_equal(gy, oy, err_msg=f"{tag}: recon Y (deblocked)")
+        np.testing.assert_array_equal(gu, ou, err_msg=f"{tag}: recon U (deblocked)")
+        np.testing.assert_array_equal(gv, ov, err_msg=f"{tag}: recon V (deblocked)")
+    ctx.close()
+
+
+@pytest.mark.parametrize("ring,q", [(4, 16), (2, 16), (4, 1), (4, 31), (3, 8)])
+def test_frames_cif(orc, cairo, ring, q):
+    _run_frames(orc, cairo, 352, 288, ring, q, 6)
+
+
+def test_frames_cif_intra_only(orc, cairo):
+    _run_frames(orc, cairo, 352, 288, 4, 16, 6, intra_only=True)
+
+
+def test_frames_odd_sizes(orc, cairo):
+    _run_frames(orc, cairo, 200, 120, 3, 16, 5)   # ragged MB grid, Wa > W
+    _run_frames(orc, cairo, 64, 48, 2, 8, 4)      # tiny: 4x3 MBs
+    _run_frames(orc, cairo, 16, 16, 2, 16, 3)     # one macroblock
+
+
+def test_frames_720p(orc, cairo):
+    _run_frames(orc, cairo, 1280, 720, 2, 16, 3)
+
+
+def test_frames_1080p_padding(orc, cairo):
+    _run_frames(orc, cairo, 1920, 1080, 4, 8, 2)  # Ha = 1088: 8 zero rows
+
+
+# ---------------------------------------------------------------------------
+# Whole streams through the drop-in encoder (evx1_encoder API)
+# ---------------------------------------------------------------------------
+
+STREAMS = json.load(open(os.path.join(GOLD, "oracle_streams.json")))["configs"]
+
+
+@pytest.mark.parametrize("cfg", STREAMS, ids=[c["name"] for c in STREAMS])
+def test_encoder_stream_matches_golden(orc, cairo, cfg):
+    enc = cairo.Encoder(ring=cfg["ring"])
+    enc.set_quality(cfg["quality"])
+    w, h = cfg["width"], cfg["height"]
+    bs = cairo.BitStream(w * h * 64 + 65536)
+    hsh = orc.FNV_OFFSET
+    for t in range(cfg["frames"]):
+        if cfg["intra_only"]:
+            enc.insert_intra()
+        bs.empty()
+        enc.encode(cairo.make_band4(w, h, t), bs)
+        n = bs.bits()
+        assert n == cfg["frame_bits"][t], f"frame {t}"
+        hsh = orc.fnv1a64(orc.canonical_frame_bytes(bs.data(), n, t == 0), hsh)
+    assert f"{hsh:016x}" == cfg["fnv1a64"]
+    enc.close()
