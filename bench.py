@@ -1,0 +1,316 @@
+"""bench.py -- encoded Mpixels/s of the EVX-1 encode hot path on MI355X.
+
+Metric (BASELINE.json): encoded Mpixels/s (p-frame, q=16), bit-exact vs ref.
+Workload (BASELINE.json configs[1]): 1280x720, p-frame with 1 reference
+(ring R = 2), quality 16, band4 synthetic content (seed 1234).
+
+A step = one P-frame through the hot path: RGB->YUV, inter search, the
+macroblock wavefront (intra search, classify, transform, VAQ, quantize,
+reconstruct), deblock, and the block table + coefficients handed to host
+memory for the entropy stage.  All input frames are resident in HBM before the
+timed region.  The host entropy stage (outside the hot path by design) is
+measured separately (end_to_end) and the output is checked bit-exact against
+the oracle on the cpu_baseline sample.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank encodes its
+own stream (the path has no cross-stream exchange), value = aggregate.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from collections import deque
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (width, height, ring, quality, BASELINE.json configs index)
+    "720p": (1280, 720, 2, 16, 1),
+    "1080p": (1920, 1080, 4, 8, 2),
+    "4k": (3840, 2160, 4, 16, 3),
+    "cif": (352, 288, 4, 16, 0),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=120)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--config", default="720p", choices=sorted(CONFIGS))
+    p.add_argument("--cpu-frames", type=int, default=48, help="P-frames in the bounded CPU baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--entropy-threads", type=int, default=8)
+    p.add_argument("--no-end-to-end", action="store_true")
+    p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
+    return p.parse_args()
+
+
+def algorithmic_bytes(w, h, ring):
+    """bytes per launch, P = one int16 YUV420 plane set."""
+    wa, ha = (w + 15) & ~15, (h + 15) & ~15
+    P = 3 * wa * ha
+    return {
+        "convert": 3 * w * h + P,
+        "inter_search": ring * P,  # source + (R-1) reference plane sets
+        "mb_rows": 5 * P,          # source, slot window, prediction, recon + coeff writes
+        "deblock": 2 * P,
+    }
+
+
+def run_hot_path(ctx, dev_frames, frame_ptr, first, count, quality, stages, entropy=None):
+    """Submit frames [first, first+count) with up to `stages` in flight."""
+    inflight = deque()
+    for f in range(first, first + count):
+        if len(inflight) == stages:
+            t = inflight.popleft()
+            out = ctx.wait(t, copy=False)
+            if entropy is not None:
+                entropy(t, out)
+            else:
+                ctx.release(t)
+        inflight.append(ctx.submit(frame_ptr(f), f, f > 0, quality, on_device=True))
+    while inflight:
+        t = inflight.popleft()
+        out = ctx.wait(t, copy=False)
+        if entropy is not None:
+            entropy(t, out)
+        else:
+            ctx.release(t)
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # device memory, barrier and max-over-ranks timing only
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import cairo_amd
+
+    w, h, ring, q, cfg_idx = CONFIGS[a.config]
+    nframes = a.warmup + a.steps
+    # synthetic input, uploaded to HBM before timing
+    host = np.empty((nframes, h, w, 3), np.uint8)
+    for f in range(nframes):
+        host[f] = cairo_amd.make_band4(w, h, f)
+    frames = torch.from_numpy(host).to(dev)
+    base, stride = frames.data_ptr(), w * h * 3
+
+    def frame_ptr(f):
+        return base + f * stride
+
+    ctx = cairo_amd.Context(w, h, ring, device=local)
+    stages = ctx.L.cairo_ctx_stages(ctx.h)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    # warmup: frame 0 (I) + P-frames 1..W-1
+    run_hot_path(ctx, frames, frame_ptr, 0, a.warmup, q, stages)
+    ctx.sync()
+    ctx.set_profiling(True)
+    ctx.take_timings()
+    barrier()
+    t0 = time.perf_counter()
+    run_hot_path(ctx, frames, frame_ptr, a.warmup, a.steps, q, stages)
+    ctx.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms, kframes = ctx.take_timings()
+    ctx.set_profiling(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pixels = w * h * a.steps * world
+    value = pixels / elapsed / 1e6
+    per_kernel = {k: kernel_ms[i] / max(kframes, 1) for i, k in enumerate(["convert", "inter_search", "mb_rows", "deblock"])}
+    abytes = algorithmic_bytes(w, h, ring)
+    dominant = max(per_kernel, key=per_kernel.get)
+
+    def roofline(kernel):
+        ms = per_kernel[kernel]
+        ach = abytes[kernel] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "algorithmic_bytes": abytes[kernel],
+                "avg_ms": round(ms, 4)}
+
+    roof = roofline(dominant)
+    roof_ms = roofline("inter_search")
+    pmc_path = a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+        for r in (roof, roof_ms):
+            k = pmc.get("per_launch_hbm_bytes", {}).get(r["kernel"])
+            if k is not None:
+                r["traffic"] = k
+                r["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+
+    # end-to-end: hot path + host entropy on worker threads (rank 0 reports)
+    e2e = None
+    if not a.no_end_to_end:
+        ctx2 = cairo_amd.Context(w, h, ring, device=local)
+        e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, barrier, dist, dev, world)
+        ctx2.close()
+
+    result = {
+        "metric": "encoded Mpixels/s (p-frame, q=16) at 1/2/4/8 MI355X; bit-exact vs ref",
+        "value": round(value, 3),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int16",
+        "data": "synthetic (band4 generator, seed 1234; SURVEY.md §8(d))",
+        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}])",
+                   "width": w, "height": h, "ring": ring, "quality": q,
+                   "parallelism": f"replicas: {world} independent stream(s), one per GPU"},
+        "roofline": roof,
+        "roofline_motion_search": roof_ms,
+        "kernels_avg_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+        "end_to_end": e2e,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, a.cpu_frames)
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, world):
+    """Hot path + host entropy (frames spread over threads), bitstreams produced."""
+    import concurrent.futures as cf
+
+    stages = ctx.L.cairo_ctx_stages(ctx.h)
+    pool = cf.ThreadPoolExecutor(max_workers=a.entropy_threads)
+    pending = {}
+    bits = {}
+    lock = threading.Lock()
+
+    def entropy(t, out):
+        # serialize_slice releases the GIL (ctypes) while it runs
+        def job(t=t, out=out):
+            _, n = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, out.coef_y, out.coef_u, out.coef_v)
+            with lock:
+                bits[t] = n
+            ctx.release(t)
+
+        pending[t] = pool.submit(job)
+        # bound in-flight entropy work to the staging depth
+        done = [k for k, fut in pending.items() if fut.done()]
+        for k in done:
+            pending.pop(k).result()
+
+    # warmup (I + P) then timed P-frames
+    run_e2e(ctx, frame_ptr, 0, a.warmup, q, stages, entropy, pending)
+    barrier()
+    t0 = time.perf_counter()
+    run_e2e(ctx, frame_ptr, a.warmup, a.steps, q, stages, entropy, pending)
+    ctx.sync()
+    barrier()
+    el = time.perf_counter() - t0
+    pool.shutdown(wait=True)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return {"value": round(w * h * a.steps * world / el / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_step": round(el * 1e3 / a.steps, 4), "entropy_threads": a.entropy_threads,
+            "staging_slots": stages,
+            "note": "hot path + host entropy (serialize_slice) pipelined; bitstreams produced"}
+
+
+def run_e2e(ctx, frame_ptr, first, count, q, stages, entropy, pending):
+    inflight = deque()
+    for f in range(first, first + count):
+        # a staging slot is free once its entropy job released it
+        while len(inflight) + len(pending) >= stages:
+            if inflight:
+                t = inflight.popleft()
+                entropy(t, ctx.wait(t, copy=False))
+            else:
+                k = next(iter(pending))
+                pending.pop(k).result()
+        inflight.append(ctx.submit(frame_ptr(f), f, f > 0, q, on_device=True))
+    while inflight:
+        t = inflight.popleft()
+        entropy(t, ctx.wait(t, copy=False))
+    for k in list(pending):
+        pending.pop(k).result()
+
+
+def cpu_baseline(cairo_amd, w, h, ring, q, pframes):
+    """The oracle (plain-C restatement of the reference encoder, test
+    infrastructure) on one host core over a bounded sample: frame 0 (I) +
+    `pframes` P-frames; P-frame Mpix/s.  The same frames are then encoded by
+    the GPU path + host entropy and compared bit for bit (the checker role)."""
+    from oracle import oracle as orc
+
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    ref = []
+    tp = 0.0
+    for t in range(pframes + 1):
+        rgb = cairo_amd.make_band4(w, h, t)
+        t0 = time.perf_counter()
+        data, n = e.encode(rgb)
+        dt = time.perf_counter() - t0
+        if t > 0:
+            tp += dt
+        ref.append(orc.canonical_frame_bytes(data, n, t == 0))
+    base = {"value": round(w * h * pframes / tp / 1e6, 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "sample": f"{w}x{h} q={q} R={ring}: frame 0 (I, untimed) + {pframes} P-frames timed, band4 seed 1234, "
+                      f"oracle/evx_oracle.c -O2, one thread"}
+    try:
+        import platform
+
+        base["cpu"] = platform.processor() or open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": ")
+    except Exception:
+        pass
+    # bit-exact check of the GPU path on the same frames (drop-in encoder API)
+    enc = cairo_amd.Encoder(ring=ring)
+    enc.set_quality(q)
+    bs = cairo_amd.BitStream(w * h * 64)
+    mism = []
+    for t in range(pframes + 1):
+        bs.empty()
+        enc.encode(cairo_amd.make_band4(w, h, t), bs)
+        if orc.canonical_frame_bytes(bs.data(), bs.bits(), t == 0) != ref[t]:
+            mism.append(t)
+    enc.close()
+    exact = {"frames_checked": pframes + 1, "mismatched_frames": mism, "bit_exact": not mism}
+    return base, exact
+
+
+if __name__ == "__main__":
+    main()

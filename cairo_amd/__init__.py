@@ -257,8 +257,8 @@ class Context:
 
 def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):
     """Host entropy stage on explicit inputs -> (bytes, nbits)."""
-    cap = capacity_bytes or (cy.size * 8 + 65536)
-    out = np.zeros(cap, np.uint8)
+    cap = capacity_bytes or (cy.size * 4 + 65536)
+    out = np.empty(cap, np.uint8)
     pos = ctypes.c_uint32(0)
     t = np.ascontiguousarray(table).view(np.uint8)
     cy, cu, cv = (np.ascontiguousarray(a, dtype=np.int16) for a in (cy, cu, cv))

@@ -25,7 +25,7 @@ using namespace cairo;
 
 namespace {
 
-constexpr int kStages = 3;
+constexpr int kStages = 8;
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,
               kInvalidResource = 8;
 
@@ -34,6 +34,8 @@ struct Stage {
   int16_t* coef = nullptr;   // pinned, 1.5 * wa * ha
   int32_t* err = nullptr;    // pinned, 1 word
   hipEvent_t k2_done = nullptr, d2h_done = nullptr;
+  hipEvent_t ev[5] = {};  // kernel boundaries of this frame (profiling)
+  bool timed = false;     // ev[] recorded, not yet collected
   int ticket = -1;
   bool busy = false;
   uint32_t index = 0, type = 0, quality = 0;
@@ -48,17 +50,15 @@ struct cairo_ctx {
   hipStream_t ks = nullptr, cs = nullptr;
   int16_t *in = nullptr, *coef = nullptr, *ring_buf = nullptr;
   BlockDesc *table = nullptr, *inter_desc = nullptr;
-  int32_t *inter_sad = nullptr, *sync = nullptr;
+  int32_t *inter_sad = nullptr, *sync = nullptr, *sticky = nullptr;
   uint8_t* rgb = nullptr;
   size_t sync_words = 0;
   Stage st[kStages];
   int next_ticket = 0;
   int wg_rows = 0, wg_deblock = 0;
   bool profiling = false;
-  hipEvent_t ev[5] = {};
   double acc_ms[4] = {0, 0, 0, 0};
   int acc_frames = 0;
-  bool pending_times = false;
   bool have_inter = false;
   int16_t* predeblock = nullptr;  // debug snapshot of the slot after K2 (opt-in)
 };
@@ -106,6 +106,7 @@ FrameArgs frame_args(const cairo_ctx* c, uint32_t index, uint32_t type, uint32_t
   a.inter_desc = c->inter_desc;
   a.inter_sad = c->inter_sad;
   a.sync = c->sync;
+  a.sticky = c->sticky;
   return a;
 }
 
@@ -120,9 +121,9 @@ void free_ctx(cairo_ctx* c) {
     if (s.err) (void)hipHostFree(s.err);
     if (s.k2_done) (void)hipEventDestroy(s.k2_done);
     if (s.d2h_done) (void)hipEventDestroy(s.d2h_done);
+    for (auto& e : s.ev)
+      if (e) (void)hipEventDestroy(e);
   }
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
   (void)hipFree(c->in);
   (void)hipFree(c->coef);
   (void)hipFree(c->ring_buf);
@@ -130,6 +131,7 @@ void free_ctx(cairo_ctx* c) {
   (void)hipFree(c->inter_desc);
   (void)hipFree(c->inter_sad);
   (void)hipFree(c->sync);
+  (void)hipFree(c->sticky);
   (void)hipFree(c->rgb);
   (void)hipFree(c->predeblock);
   if (c->ks) (void)hipStreamDestroy(c->ks);
@@ -192,6 +194,8 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   TRY(hipMalloc(&c->inter_desc, nref * mbs * sizeof(BlockDesc)));
   TRY(hipMalloc(&c->inter_sad, nref * mbs * sizeof(int32_t)));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t)));
+  TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
+  TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3));
   for (auto& s : c->st) {
     TRY(hipHostMalloc(&s.table, mbs * sizeof(BlockDesc), hipHostMallocDefault));
@@ -199,8 +203,8 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
     TRY(hipHostMalloc(&s.err, sizeof(int32_t), hipHostMallocDefault));
     TRY(hipEventCreateWithFlags(&s.k2_done, hipEventDisableTiming));
     TRY(hipEventCreateWithFlags(&s.d2h_done, hipEventDisableTiming));
+    for (auto& e : s.ev) TRY(hipEventCreate(&e));
   }
-  for (auto& e : c->ev) TRY(hipEventCreate(&e));
 #undef TRY
   r = zero_state(c);
   if (r != kSuccess) {
@@ -240,24 +244,26 @@ int cairo_ctx_set_profiling(cairo_ctx* c, int enable) {
   return kSuccess;
 }
 
-static int collect_times(cairo_ctx* c) {
-  if (!c->pending_times) return kSuccess;
-  CK(hipEventSynchronize(c->ev[4]));
+static int collect_times(cairo_ctx* c, Stage& s) {
+  if (!s.timed) return kSuccess;
+  CK(hipEventSynchronize(s.ev[4]));
   for (int k = 0; k < 4; k++) {
     float ms = 0;
-    CK(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
+    CK(hipEventElapsedTime(&ms, s.ev[k], s.ev[k + 1]));
     c->acc_ms[k] += ms;
   }
   c->acc_frames++;
-  c->pending_times = false;
+  s.timed = false;
   return kSuccess;
 }
 
 int cairo_ctx_take_timings(cairo_ctx* c, double ms[4], int* frames) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  int r = collect_times(c);
-  if (r) return r;
+  for (auto& s : c->st) {
+    int r = collect_times(c, s);
+    if (r) return r;
+  }
   for (int k = 0; k < 4; k++) {
     if (ms) ms[k] = c->acc_ms[k];
     c->acc_ms[k] = 0;
@@ -277,8 +283,8 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
     fprintf(stderr, "[cairo_amd] staging slot of ticket %d not released\n", s.ticket);
     return kInvalidResource;
   }
-  if (c->profiling) {
-    int r = collect_times(c);  // events are reused per frame
+  {
+    int r = collect_times(c, s);  // this stage's events are about to be reused
     if (r) return r;
   }
   FrameArgs a = frame_args(c, index, type, quality);
@@ -287,34 +293,35 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   } else {
     CK(hipMemcpyAsync(c->rgb, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, c->ks));
   }
-  CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t), c->ks));
-  if (c->profiling) CK(hipEventRecord(c->ev[0], c->ks));
-  CK(launch_convert(a, c->ks));
-  if (c->profiling) CK(hipEventRecord(c->ev[1], c->ks));
-  if (a.inter && c->ring > 1) CK(launch_inter_search(a, c->ks));
-  c->have_inter = a.inter && c->ring > 1;
-  if (c->profiling) CK(hipEventRecord(c->ev[2], c->ks));
-  // K2 rewrites the coefficient planes: the previous frame's D2H must be done.
+  // K2 rewrites the coefficient planes and the block table, and the memset
+  // below clears the error word: the previous frame's D2H must have finished.
   const Stage& prev = c->st[(t + kStages - 1) % kStages];
   if (prev.ticket >= 0) CK(hipStreamWaitEvent(c->ks, prev.d2h_done, 0));
+  CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t), c->ks));
+  const bool prof = c->profiling;
+  if (prof) CK(hipEventRecord(s.ev[0], c->ks));
+  CK(launch_convert(a, c->ks));
+  if (prof) CK(hipEventRecord(s.ev[1], c->ks));
+  if (a.inter && c->ring > 1) CK(launch_inter_search(a, c->ks));
+  c->have_inter = a.inter && c->ring > 1;
+  if (prof) CK(hipEventRecord(s.ev[2], c->ks));
   CK(launch_mb_rows(a, c->wg_rows, c->ks));
-  if (c->profiling) CK(hipEventRecord(c->ev[3], c->ks));
+  if (prof) CK(hipEventRecord(s.ev[3], c->ks));
   CK(hipEventRecord(s.k2_done, c->ks));
   if (c->predeblock)
     CK(hipMemcpyAsync(c->predeblock, c->ring_buf + (size_t)(index % c->ring) * c->plane_elems,
                       c->plane_elems * 2, hipMemcpyDeviceToDevice, c->ks));
   CK(launch_deblock(a, c->wg_deblock, c->ks));
-  if (c->profiling) {
-    CK(hipEventRecord(c->ev[4], c->ks));
-    c->pending_times = true;
+  if (prof) {
+    CK(hipEventRecord(s.ev[4], c->ks));
+    s.timed = true;
   }
   // Outputs for the host entropy stage.
   const size_t mbs = (size_t)c->wmb * c->hmb;
   CK(hipStreamWaitEvent(c->cs, s.k2_done, 0));
   CK(hipMemcpyAsync(s.table, c->table, mbs * sizeof(BlockDesc), hipMemcpyDeviceToHost, c->cs));
   CK(hipMemcpyAsync(s.coef, c->coef, c->plane_elems * 2, hipMemcpyDeviceToHost, c->cs));
-  CK(hipMemcpyAsync(s.err, c->sync + SyncLayout::kErr, sizeof(int32_t), hipMemcpyDeviceToHost,
-                    c->cs));
+  CK(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
   CK(hipEventRecord(s.d2h_done, c->cs));
   s.busy = true;
   s.ticket = t;
@@ -333,7 +340,7 @@ int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
   CK(hipSetDevice(c->device));
   CK(hipEventSynchronize(s.d2h_done));
   if (*s.err) {
-    fprintf(stderr, "[cairo_amd] in-kernel wait timed out (frame %u)\n", s.index);
+    fprintf(stderr, "[cairo_amd] an in-kernel wait timed out (at or before frame %u)\n", s.index);
     return kHardwareFail;
   }
   out->block_table = s.table;

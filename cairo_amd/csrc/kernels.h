@@ -43,6 +43,7 @@ struct FrameArgs {
   BlockDesc* inter_desc;   // [(off-1)*mbs + mb]
   int32_t* inter_sad;      // [(off-1)*mbs + mb]
   int32_t* sync;           // SyncLayout words, zeroed before every frame
+  int32_t* sticky;         // timeout flag that is never cleared (reported by the host)
 };
 
 // Words of FrameArgs::sync (all int32, zeroed per frame).

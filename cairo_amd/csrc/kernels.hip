@@ -73,7 +73,8 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
 // timeout (~2 s) the error word is set and the wait gives up, so every
 // workgroup still drains and the host reports EVX_ERROR_HARDWAREFAIL.
-__device__ __forceinline__ void wait_at_least(int32_t* word, int target, int32_t* err) {
+__device__ __forceinline__ void wait_at_least(int32_t* word, int target, int32_t* err,
+                                              int32_t* sticky) {
   if (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -81,6 +82,7 @@ __device__ __forceinline__ void wait_at_least(int32_t* word, int target, int32_t
     __builtin_amdgcn_s_sleep(2);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
   }
@@ -565,7 +567,7 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
       if (by > 0) {
-        if (threadIdx.x == 0) wait_at_least(&done[by - 1], min(bx + 3, a.wmb), err);
+        if (threadIdx.x == 0) wait_at_least(&done[by - 1], min(bx + 3, a.wmb), err, a.sticky);
         acquire_after_wait();
       }
       // Stage the current slot around the MB: x in [px-32, px+48), y in [py-48, py+32).
@@ -806,7 +808,7 @@ __global__ __launch_bounds__(256) void k_deblock(FrameArgs a) {
     for (int c = 0; c < nx; c += kDbChunk) {
       const int cend = min(c + kDbChunk, nx);
       if (band > 0) {
-        if (threadIdx.x == 0) wait_at_least(&prog[band - 1], min(cend + 1, nx), err);
+        if (threadIdx.x == 0) wait_at_least(&prog[band - 1], min(cend + 1, nx), err, a.sticky);
         acquire_after_wait();
         // horizontal edges H(x, j), x in [c, cend): column filters
         const int x = c + (threadIdx.x >> 3);
