@@ -73,6 +73,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_read_table": (I, [P, P]),
         "cairo_ctx_set_debug": (I, [P, I]),
         "cairo_ctx_read_predeblock": (I, [P, P, P, P]),
+        "cairo_ctx_read_stamps": (I, [P, P]),
         "cairo_ctx_set_profiling": (I, [P, I]),
         "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
         "cairo_ctx_set_workgroups": (I, [P, I, I]),
@@ -241,6 +242,11 @@ class Context:
         v = np.empty_like(u)
         _ck(self.L.cairo_ctx_read_predeblock(self.h, _ptr(y), _ptr(u), _ptr(v)), "read_predeblock")
         return y, u, v
+
+    def read_stamps(self) -> np.ndarray:
+        out = np.zeros((self.hmb, self.wmb, 10), np.uint64)
+        _ck(self.L.cairo_ctx_read_stamps(self.h, _ptr(out)), "read_stamps")
+        return out
 
     def set_profiling(self, enable: bool) -> None:
         _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")

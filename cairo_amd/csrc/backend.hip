@@ -61,6 +61,7 @@ struct cairo_ctx {
   int acc_frames = 0;
   bool have_inter = false;
   int16_t* predeblock = nullptr;  // debug snapshot of the slot after K2 (opt-in)
+  uint64_t* stamps = nullptr;     // diagnostic K2 phase stamps (opt-in)
 };
 
 namespace {
@@ -107,6 +108,7 @@ FrameArgs frame_args(const cairo_ctx* c, uint32_t index, uint32_t type, uint32_t
   a.inter_sad = c->inter_sad;
   a.sync = c->sync;
   a.sticky = c->sticky;
+  a.stamps = c->stamps;
   return a;
 }
 
@@ -134,6 +136,7 @@ void free_ctx(cairo_ctx* c) {
   (void)hipFree(c->sticky);
   (void)hipFree(c->rgb);
   (void)hipFree(c->predeblock);
+  (void)hipFree(c->stamps);
   if (c->ks) (void)hipStreamDestroy(c->ks);
   if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
@@ -402,6 +405,17 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
   if ((flags & 1) && !c->predeblock) CK(hipMalloc(&c->predeblock, c->plane_elems * 2));
+  if ((flags & 2) && !c->stamps)
+    CK(hipMalloc(&c->stamps, (size_t)c->wmb * c->hmb * kStampPhases * sizeof(uint64_t)));
+  return kSuccess;
+}
+
+int cairo_ctx_read_stamps(cairo_ctx* c, uint64_t* out) {
+  if (!c || !c->stamps || !out) return kInvalidArg;
+  CK(hipSetDevice(c->device));
+  CK(hipStreamSynchronize(c->ks));
+  CK(hipMemcpy(out, c->stamps, (size_t)c->wmb * c->hmb * kStampPhases * sizeof(uint64_t),
+               hipMemcpyDeviceToHost));
   return kSuccess;
 }
 

@@ -44,7 +44,11 @@ struct FrameArgs {
   int32_t* inter_sad;      // [(off-1)*mbs + mb]
   int32_t* sync;           // SyncLayout words, zeroed before every frame
   int32_t* sticky;         // timeout flag that is never cleared (reported by the host)
+  uint64_t* stamps;        // diagnostic: per-MB phase timestamps (nullptr = off)
 };
+
+// Phase boundaries recorded per macroblock by k_mb_rows when stamps != nullptr.
+constexpr int kStampPhases = 10;
 
 // Words of FrameArgs::sync (all int32, zeroed per frame).
 struct SyncLayout {

@@ -70,6 +70,12 @@ __device__ __forceinline__ int wave_max(int v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Diagnostic timestamp (100 MHz constant clock) of phase k of macroblock mb.
+__device__ __forceinline__ void stamp(const FrameArgs& a, int mb, int k) {
+  if (a.stamps && threadIdx.x == 0)
+    a.stamps[(size_t)mb * kStampPhases + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 // Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
 // timeout (~2 s) the error word is set and the wait gives up, so every
 // workgroup still drains and the host reports EVX_ERROR_HARDWAREFAIL.
@@ -390,6 +396,7 @@ hipError_t launch_inter_search(const FrameArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 
 constexpr int kMBElems = 384;
+typedef short int8v __attribute__((ext_vector_type(8)));
 
 // Pixel coordinates of element e of the macroblock whose luma origin is (x, y):
 // plane 0/1/2 and (px, py) inside that plane.
@@ -406,80 +413,76 @@ __device__ __forceinline__ void elem_coords(int e, int x, int y, int& plane, int
   }
 }
 
-// Forward row pass (transform_8x8_line_fast along rows) then column pass;
-// intermediate stored as int16.  in -> out, scratch tmp.  256 threads.
-__device__ void fdct_mb(const int16_t* in, int16_t* tmp, int16_t* out) {
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    int b = e >> 6, r = (e >> 3) & 7, i = e & 7;
-    const int16_t* row = in + b * 64 + r * 8;
-    int t = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) t += row[k] * kLut8[i * 8 + k];
-    t = i == 0 ? (t * 45) / 128 : t / 2;
-    tmp[e] = (int16_t)rdiv(t, 128);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    int b = e >> 6, i = (e >> 3) & 7, c = e & 7;
-    const int16_t* col = tmp + b * 64 + c;
-    int t = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) t += col[k * 8] * kLut8[i * 8 + k];
-    t = i == 0 ? (t * 45) / 128 : t / 2;
-    out[e] = (int16_t)rdiv(t, 128);
-  }
-  __syncthreads();
+// One 8x8 block per wave, one element per lane (lane = r*8 + c).  LDS scratch
+// a/b (64 int16 each) carry the passes; the wave's LDS operations execute in
+// order, so no workgroup barrier is needed.
+
+__device__ __forceinline__ int8v load_row8(const int16_t* p) {  // 8 int16, 16-B aligned
+  return *(const int8v*)p;
 }
 
-// Inverse: column pass then row pass (inverse_transform_8x8_line_fast, per-term
-// truncation); the row pass adds pred when add != 0 (int16 result, unclamped).
-__device__ void idct_mb(const int16_t* in, int16_t* tmp, const int16_t* pred, bool add,
-                        int16_t* out) {
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    int b = e >> 6, i = (e >> 3) & 7, c = e & 7;
-    const int16_t* col = in + b * 64 + c;
-    int t = ((col[0] * kLut8[i]) * 45) / 128;
+// transform_8x8 (transform.cpp:264-301): rows, int16 scratch, then columns.
+// x = this lane's residual (r, c); returns its coefficient (r, c).
+__device__ __forceinline__ int fdct_lane(int16_t* sa, int16_t* sb, int lane, int16_t x) {
+  const int r8 = lane >> 3, c8 = lane & 7;
+  sa[lane] = x;
+  __builtin_amdgcn_wave_barrier();
+  {
+    const int8v row = load_row8(&sa[r8 * 8]);
+    int t = 0;
 #pragma unroll
-    for (int k = 1; k < 8; k++) t += (col[k * 8] * kLut8[k * 8 + i]) / 2;
-    tmp[e] = (int16_t)rdiv(t, 128);
+    for (int k = 0; k < 8; k++) t += row[k] * kLut8[c8 * 8 + k];
+    t = c8 == 0 ? (t * 45) / 128 : t / 2;
+    sb[c8 * 8 + r8] = (int16_t)rdiv(t, 128);  // transposed
   }
-  __syncthreads();
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    int b = e >> 6, r = (e >> 3) & 7, i = e & 7;
-    const int16_t* row = tmp + b * 64 + r * 8;
-    int t = ((row[0] * kLut8[i]) * 45) / 128;
+  __builtin_amdgcn_wave_barrier();
+  const int8v col = load_row8(&sb[c8 * 8]);  // column c8 of the row pass
+  int t = 0;
 #pragma unroll
-    for (int k = 1; k < 8; k++) t += (row[k] * kLut8[k * 8 + i]) / 2;
-    t = rdiv(t, 128);
-    out[e] = (int16_t)(add ? t + pred[e] : t);
-  }
-  __syncthreads();
+  for (int k = 0; k < 8; k++) t += col[k] * kLut8[r8 * 8 + k];
+  t = r8 == 0 ? (t * 45) / 128 : t / 2;
+  return (int16_t)rdiv(t, 128);
 }
 
-// variance2 of the 16x16 luma coefficients (analysis.h:176-198): skip only the
-// first coefficient of the top-left quadrant; wrapping int32 arithmetic.
-// Threads 0..255 hold one luma coefficient each.  Returns a uniform value.
-__device__ int32_t variance2_mb(const int16_t* coef, int32_t* red /* LDS, 12 words */) {
-  int e = threadIdx.x;  // < 256: luma
-  int32_t t = coef[e];
-  bool use = e != 0 && t != 0;
-  uint32_t sum = use ? (uint32_t)t : 0u, sq = use ? (uint32_t)(t * t) : 0u;
-  int cnt = use ? 1 : 0;
-  int ws = wave_sum((int)sum), wq = wave_sum((int)sq), wc = wave_sum(cnt);
-  int w = threadIdx.x >> 6;
-  if (lane_id() == 0) {
-    red[w] = ws;
-    red[4 + w] = wq;
-    red[8 + w] = wc;
+// inverse_transform_8x8 (transform.cpp:330-366): columns then rows, per-term
+// truncation.  d = this lane's dequantized coefficient (r, c); returns the
+// inverse-transformed sample (r, c) before the prediction is added.
+__device__ __forceinline__ int idct_lane(int16_t* sa, int16_t* sb, int lane, int16_t d) {
+  const int r8 = lane >> 3, c8 = lane & 7;
+  sa[c8 * 8 + r8] = d;  // transposed: row c8 of sa = column c8
+  __builtin_amdgcn_wave_barrier();
+  {
+    const int8v col = load_row8(&sa[c8 * 8]);
+    int t = ((col[0] * kLut8[r8]) * 45) / 128;
+#pragma unroll
+    for (int k = 1; k < 8; k++) t += (col[k] * kLut8[k * 8 + r8]) / 2;
+    sb[r8 * 8 + c8] = (int16_t)rdiv(t, 128);
   }
+  __builtin_amdgcn_wave_barrier();
+  const int8v row = load_row8(&sb[r8 * 8]);
+  int t = ((row[0] * kLut8[c8]) * 45) / 128;
+#pragma unroll
+  for (int k = 1; k < 8; k++) t += (row[k] * kLut8[k * 8 + c8]) / 2;
+  return rdiv(t, 128);
+}
+
+// VAQ over the 16x16 luma coefficients (analysis.h:176-198, quantize.cpp:60-77):
+// wave w holds luma quadrant w; the first coefficient of quadrant 0 is skipped;
+// wrapping int32 arithmetic.  Contains one workgroup barrier; returns
+// (qp, variance2) uniform across the workgroup.
+__device__ __forceinline__ int vaq_mb(int32_t* red, int wave, int lane, int coef, int quality,
+                                      int32_t* var_out) {
+  const bool use = !(wave == 0 && lane == 0) && coef != 0;
+  const int ws = wave_sum(use ? coef : 0), wq = wave_sum(use ? coef * coef : 0),
+            wc = wave_sum(use ? 1 : 0);
+  if (lane == 0) red[wave] = ws, red[4 + wave] = wq, red[8 + wave] = wc;
   __syncthreads();
-  uint32_t S = (uint32_t)red[0] + (uint32_t)red[1] + (uint32_t)red[2] + (uint32_t)red[3];
-  uint32_t Q = (uint32_t)red[4] + (uint32_t)red[5] + (uint32_t)red[6] + (uint32_t)red[7];
-  int32_t C = red[8] + red[9] + red[10] + red[11];
-  __syncthreads();
-  if (C <= 0) return 0;
-  int32_t sq2 = (int32_t)(S * S);
-  return (int32_t)(Q - (uint32_t)rdiv(sq2, C));
+  const uint32_t S = (uint32_t)red[0] + (uint32_t)red[1] + (uint32_t)red[2] + (uint32_t)red[3];
+  const uint32_t Q = (uint32_t)red[4] + (uint32_t)red[5] + (uint32_t)red[6] + (uint32_t)red[7];
+  const int32_t C = red[8] + red[9] + red[10] + red[11];
+  const int32_t v2 = C > 0 ? (int32_t)(Q - (uint32_t)rdiv((int32_t)(S * S), C)) : 0;
+  *var_out = v2;
+  return (int)vaq_from_variance((uint32_t)quality, v2);
 }
 
 // quantize_macroblock (quantize.cpp:357-367): element-wise.
@@ -502,152 +505,269 @@ __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool i
   return (int16_t)(((2 * v) * kQmInter[k] * qp) / kQScale);
 }
 
-// Shared per-macroblock encode/reconstruct chain (encode_block + decode_block
-// for the non-copy types): residual -> fdct -> VAQ -> quantize -> dequantize ->
-// idct (+pred).  src/pred/res/tmp/coef/rec are LDS arrays of 384.
-// Returns q_index; variance via *var.
-__device__ uint32_t code_mb(const int16_t* src, const int16_t* pred, uint32_t type, int quality,
-                            int16_t* res, int16_t* tmp, int16_t* coef, int16_t* qc,
-                            int16_t* rec, int32_t* red, int32_t* var) {
-  const bool has_pred = type != kIntra;  // INTRA_DEFAULT transforms the source
-  for (int e = threadIdx.x; e < kMBElems; e += 256)
-    res[e] = has_pred ? (int16_t)(src[e] - pred[e]) : src[e];
-  __syncthreads();
-  fdct_mb(res, tmp, coef);
-  int32_t v2 = variance2_mb(coef, red);
-  uint32_t qp = vaq_from_variance((uint32_t)quality, v2);
-  *var = v2;
-  const bool intra_path = (type & kIntra) && !(type & kMotion);
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    int16_t q = quant_elem(e, coef[e], (int)qp, intra_path);
-    qc[e] = q;
-    res[e] = dequant_elem(e, q, (int)qp, intra_path);
-  }
-  __syncthreads();
-  idct_mb(res, tmp, pred, has_pred, rec);
-  return qp;
-}
-
 // ---------------------------------------------------------------------------
 // K2: the macroblock wavefront.  One workgroup owns one macroblock row at a
 // time (dequeued in order) and walks it left to right.  MB (bx, by) starts
 // when row by-1 has finished MB bx+2, i.e. the schedule t = bx + 3*by that
 // reproduces the raster order's reads of in-progress (rows above, left) and
 // stale (row below, frame n-R) reconstruction bit for bit.
+//
+// The current slot around the row lives in a circular LDS window: MB rows
+// by-3..by+1 (80 pixel rows) by 128 columns addressed with absolute x & 127.
+// A step loads only the new column (rows by-3..by-1 at bx+2) and one stale
+// macroblock (row by+1 at bx-1); the row's own reconstruction is written
+// straight into the window.
 // ---------------------------------------------------------------------------
 
-struct alignas(16) MbLds {
-  Window win;
-  int16_t src[kMBElems], pred[kMBElems], res[kMBElems], tmp[kMBElems], coef[kMBElems],
-      qc[kMBElems], rec[kMBElems];
-  int32_t cand[2][16][2];  // double-buffered candidate (sad, mad)
+constexpr int kCwLP = 130;  // luma window pitch (elements): 128 columns, odd dword stride
+constexpr int kCwCP = 66;   // chroma window pitch: 64 columns
+
+struct alignas(16) RowWindow {
+  int16_t y[80 * kCwLP];
+  int16_t u[40 * kCwCP];
+  int16_t v[40 * kCwCP];
+};
+
+struct alignas(16) RowLds {
+  RowWindow win;
+  int16_t bufA[kMBElems], bufB[kMBElems];  // per-block transform scratch, block-major
+  int32_t cand[2][16][2];                  // double-buffered candidate (sad, mad)
   int32_t red[12];
   int slot;
 };
 
-// Evaluate candidate c of a 3x3 step (j outer, i inner) for the intra search.
+// Move dword k (0..191) of macroblock (mbx, mby) of plane set p into the window.
+__device__ __forceinline__ void win_put(RowWindow& w, const PlaneSet& p, int wa, int oy, int mbx,
+                                        int mby, int k) {
+  if (k < 128) {
+    const int r = k >> 3, d = k & 7;
+    const int gy = mby * 16 + r, gx = mbx * 16 + 2 * d;
+    const uint32_t v = *(const uint32_t*)(p.y + (size_t)gy * wa + gx);
+    *(uint32_t*)&w.y[(gy - oy) * kCwLP + (gx & 127)] = v;
+  } else {
+    const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
+    const int gy = mby * 8 + r, gx = mbx * 8 + 2 * d;
+    const int16_t* s = (pl ? p.v : p.u) + (size_t)gy * (wa >> 1) + gx;
+    int16_t* dst = pl ? w.v : w.u;
+    *(uint32_t*)&dst[(gy - (oy >> 1)) * kCwCP + (gx & 63)] = *(const uint32_t*)s;
+  }
+}
+
+// Load a list of macroblocks (n <= 9) into the window; all threads.
+__device__ __forceinline__ void win_load(RowWindow& w, const PlaneSet& p, int wa, int oy,
+                                         const int* mbx, const int* mby, int n) {
+  for (int k = threadIdx.x; k < n * 192; k += 256) {
+    const int i = k / 192;
+    win_put(w, p, wa, oy, mbx[i], mby[i], k - i * 192);
+  }
+}
+
+// Sum / max over one 16-lane DPP row (a candidate's group); all 16 lanes get it.
+__device__ __forceinline__ int row16_sum(int v) {
+  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x122, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x121, 0xF, 0xF, false);
+  return v;
+}
+__device__ __forceinline__ int row16_max(int v) {
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x122, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x121, 0xF, 0xF, false));
+  return v;
+}
+
+// A 16-lane group evaluates one candidate: lane i owns luma row i (16 px) and
+// 4 pixels of U and V (row i>>1, columns (i&1)*4..+3).
+struct SrcRow {
+  int y[16], u[4], v[4];
+};
+
+__device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int cy, int i,
+                                         const SrcRow& s, int& sad, int& mad) {
+  const int16_t* row = &w.y[(cy + i - oy) * kCwLP];
+  int sm = 0, mx = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int d = abs(s.y[k] - row[(cx + k) & 127]);
+    sm += d;
+    mx = max(mx, d);
+  }
+  const int cr = (cy >> 1) + (i >> 1) - (oy >> 1), cc = (cx >> 1) + (i & 1) * 4;
+  const int16_t* ru = &w.u[cr * kCwCP];
+  const int16_t* rv = &w.v[cr * kCwCP];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    mx = max(mx, abs(s.u[k] - ru[(cc + k) & 63]));
+    mx = max(mx, abs(s.v[k] - rv[(cc + k) & 63]));
+  }
+  sad = row16_sum(sm);
+  mad = row16_max(mx);
+}
+
+// Sub-pel candidate: lerp of the best block (bx, by) toward neighbour (tx, ty).
+__device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, int by, int tx,
+                                           int ty, int q, int i, const SrcRow& s, int& sad,
+                                           int& mad) {
+  const int16_t* ra = &w.y[(by + i - oy) * kCwLP];
+  const int16_t* rb = &w.y[(ty + i - oy) * kCwLP];
+  int sm = 0, mx = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int d = abs(s.y[k] - lerp_px(ra[(bx + k) & 127], rb[(tx + k) & 127], q));
+    sm += d;
+    mx = max(mx, d);
+  }
+  const int ca = (by >> 1) + (i >> 1) - (oy >> 1), cb = (ty >> 1) + (i >> 1) - (oy >> 1);
+  const int xa = (bx >> 1) + (i & 1) * 4, xb = (tx >> 1) + (i & 1) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    mx = max(mx, abs(s.u[k] - lerp_px(w.u[ca * kCwCP + ((xa + k) & 63)],
+                                      w.u[cb * kCwCP + ((xb + k) & 63)], q)));
+    mx = max(mx, abs(s.v[k] - lerp_px(w.v[ca * kCwCP + ((xa + k) & 63)],
+                                      w.v[cb * kCwCP + ((xb + k) & 63)], q)));
+  }
+  sad = row16_sum(sm);
+  mad = row16_max(mx);
+}
+
 __device__ __forceinline__ bool intra_valid(int cx, int cy, int px, int py, int wa, int ha) {
   if (cy > py - kMB && cx > px - kMB) return false;  // not yet coded (motion.cpp:239-243)
   return in_frame(cx, cy, wa, ha);
 }
 
+// Pixel (ex, ey) of plane pl (0 Y, 1 U, 2 V) from the window.
+__device__ __forceinline__ int win_px(const RowWindow& w, int oy, int pl, int ex, int ey) {
+  if (pl == 0) return w.y[(ey - oy) * kCwLP + (ex & 127)];
+  const int16_t* t = pl == 1 ? w.u : w.v;
+  return t[(ey - (oy >> 1)) * kCwCP + (ex & 63)];
+}
+
+__device__ __forceinline__ const int16_t* plane_of(const PlaneSet& p, int pl) {
+  return pl == 0 ? p.y : (pl == 1 ? p.u : p.v);
+}
+
 __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
-  __shared__ MbLds L;
-  const int wave = threadIdx.x >> 6;
+  __shared__ RowLds L;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
-  const int cur = a.index % a.ring;
-  const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, cur);
+  const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
   int32_t* err = a.sync + SyncLayout::kErr;
   int32_t* done = a.sync + SyncLayout::kRowDone;
+  const int cw = a.wa >> 1;
 
   for (;;) {
     const int by = dequeue(a.sync + SyncLayout::kRowTicket, &L.slot);
     if (by >= a.hmb) break;
-    const int py = by * kMB;
+    const int py = by * kMB, oy = py - 48;
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
-      if (by > 0) {
-        if (threadIdx.x == 0) wait_at_least(&done[by - 1], min(bx + 3, a.wmb), err, a.sticky);
-        acquire_after_wait();
+      stamp(a, mb, 0);
+      // ---- window maintenance ----
+      int lx[9], ly[9], n = 0;
+      if (bx > 0) {  // older rows of the new column, and the stale block of row by+1
+        for (int r = by - 3; r <= by - 2; r++)
+          if (r >= 0 && bx + 2 < a.wmb) lx[n] = bx + 2, ly[n++] = r;
+        if (by + 1 < a.hmb) lx[n] = bx - 1, ly[n++] = by + 1;
+        win_load(L.win, cs, a.wa, oy, lx, ly, n);
+        n = 0;
       }
-      // Stage the current slot around the MB: x in [px-32, px+48), y in [py-48, py+32).
-      const int ox = px - 32, oy = py - 48;
-      load_window(L.win, cs, a.wa, a.ha, ox, oy, 256);
-      for (int e = threadIdx.x; e < kMBElems; e += 256) {
-        int pl, ex, ey;
-        elem_coords(e, px, py, pl, ex, ey);
-        const int16_t* p = pl == 0 ? a.in.y : (pl == 1 ? a.in.u : a.in.v);
-        L.src[e] = p[(size_t)ey * (pl ? a.wa >> 1 : a.wa) + ex];
+      if (by > 0) {
+        if (tid == 0) wait_at_least(&done[by - 1], min(bx + 3, a.wmb), err, a.sticky);
+        acquire_after_wait();
+        if (bx == 0) {
+          for (int r = max(by - 3, 0); r <= by - 1; r++)
+            for (int c = 0; c <= 2 && c < a.wmb; c++) lx[n] = c, ly[n++] = r;
+        } else if (bx + 2 < a.wmb) {
+          lx[n] = bx + 2, ly[n++] = by - 1;
+        }
+        win_load(L.win, cs, a.wa, oy, lx, ly, n);
+      }
+      stamp(a, mb, 1);
+      // source rows of this lane's group slot
+      SrcRow s;
+      {
+        const int8v r0 = load_row8(a.in.y + (size_t)(py + gi) * a.wa + px);
+        const int8v r1 = load_row8(a.in.y + (size_t)(py + gi) * a.wa + px + 8);
+#pragma unroll
+        for (int k = 0; k < 8; k++) s.y[k] = r0[k], s.y[8 + k] = r1[k];
+        const size_t co = (size_t)((py >> 1) + (gi >> 1)) * cw + (px >> 1) + (gi & 1) * 4;
+        const short4 u4 = *(const short4*)(a.in.u + co), v4 = *(const short4*)(a.in.v + co);
+        s.u[0] = u4.x, s.u[1] = u4.y, s.u[2] = u4.z, s.u[3] = u4.w;
+        s.v[0] = v4.x, s.v[1] = v4.y, s.v[2] = v4.z, s.v[3] = v4.w;
       }
       __syncthreads();
+      stamp(a, mb, 2);
 
       // ---- intra search (calculate_intra_prediction, motion.cpp:354-419) ----
-      const Px6 src6 = px_from_planes(a.in, a.wa, px, py);
-      Sel s;
-      s.bx = px;
-      s.by = py;
-      s.sad = wave_sum(abs(src6.y0) + abs(src6.y1) + abs(src6.y2) + abs(src6.y3));
-      s.mad = INT32_MAX;
-      s.ssd = INT32_MAX;
-      s.sp_idx = s.sp_amt = s.sp_en = 0;
+      Sel sel;
+      {
+        int sm = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) sm += abs(s.y[k]);
+        sel.sad = row16_sum(sm);  // compute_block_sad(src): every group holds the total
+      }
+      sel.bx = px;
+      sel.by = py;
+      sel.mad = INT32_MAX;
+      sel.ssd = INT32_MAX;
+      sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
       int buf = 0;
       for (int stage = 0; stage < 5; stage++) {
         const int step = stage == 0 ? kRadius : (kRadius >> stage);
-        const int bx0 = s.bx, by0 = s.by;
-        // candidate c: j = jlo + (c/3)*step, i = -step + (c%3)*step
         const int jlo = stage == 0 ? -2 * kRadius : -step;
-        for (int c = wave; c < 9; c += 4) {
-          const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
+        const int bx0 = sel.bx, by0 = sel.by;
+        if (grp < 9) {
+          const int cx = bx0 - step + (grp % 3) * step, cy = by0 + jlo + (grp / 3) * step;
           int sad = -1, mad = -1;
-          if (intra_valid(cx, cy, px, py, a.wa, a.ha))
-            sad_mad(src6, px_from_window(L.win, cx - ox, cy - oy), sad, mad);
-          if (lane_id() == 0) {
-            L.cand[buf][c][0] = sad;
-            L.cand[buf][c][1] = mad;
+          if (intra_valid(cx, cy, px, py, a.wa, a.ha)) cand_row(L.win, oy, cx, cy, gi, s, sad, mad);
+          if (gi == 0) {
+            L.cand[buf][grp][0] = sad;
+            L.cand[buf][grp][1] = mad;
           }
         }
         __syncthreads();
+        int cs_[9][2];
+#pragma unroll
+        for (int c = 0; c < 9; c++) cs_[c][0] = L.cand[buf][c][0], cs_[c][1] = L.cand[buf][c][1];
+#pragma unroll
         for (int c = 0; c < 9; c++) {
-          const int sad = L.cand[buf][c][0];
-          if (sad < 0) continue;
+          if (cs_[c][0] < 0) continue;
           const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
-          accept_int(s, cx, cy, sad, L.cand[buf][c][1], px, py, thr);
+          accept_int(sel, cx, cy, cs_[c][0], cs_[c][1], px, py, thr);
         }
         buf ^= 1;
       }
+      stamp(a, mb, 3);
       {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
-        const int bx0 = s.bx, by0 = s.by;
-        const Px6 best = px_from_window(L.win, bx0 - ox, by0 - oy);
-        for (int n = wave; n < 8; n += 4) {
-          const int k = n < 4 ? n : n + 1;  // skip the centre of the 3x3
-          const int i = k % 3 - 1, j = k / 3 - 1;
-          const int tx = bx0 + i, ty = by0 + j;
-          const bool ok = intra_valid(tx, ty, px, py, a.wa, a.ha);
-          Px6 nb;
-          if (ok) nb = px_from_window(L.win, tx - ox, ty - oy);
-          for (int q = 0; q < 2; q++) {
-            int sad = -1, mad = -1;
-            if (ok) sad_mad(src6, lerp6(best, nb, q), sad, mad);
-            if (lane_id() == 0) {
-              L.cand[buf][2 * n + q][0] = sad;
-              L.cand[buf][2 * n + q][1] = mad;
-            }
-          }
+        const int bx0 = sel.bx, by0 = sel.by;
+        const int nn = grp >> 1, q = grp & 1;
+        const int k9 = nn < 4 ? nn : nn + 1;  // skip the centre of the 3x3
+        const int tx = bx0 + k9 % 3 - 1, ty = by0 + k9 / 3 - 1;
+        int sad = -1, mad = -1;
+        if (intra_valid(tx, ty, px, py, a.wa, a.ha))
+          subpel_row(L.win, oy, bx0, by0, tx, ty, q, gi, s, sad, mad);
+        if (gi == 0) {
+          L.cand[buf][grp][0] = sad;
+          L.cand[buf][grp][1] = mad;
         }
         __syncthreads();
-        s.sp_idx = s.sp_amt = s.sp_en = 0;
-        for (int n = 0; n < 8; n++) {
-          const int k = n < 4 ? n : n + 1;
-          const int idx = frac_index(k % 3 - 1, k / 3 - 1);
-          for (int q = 0; q < 2; q++) {
-            const int sad = L.cand[buf][2 * n + q][0];
-            if (sad < 0) continue;
-            accept_sub(s, idx, q, sad, L.cand[buf][2 * n + q][1], thr);
-          }
+        int cs_[16][2];
+#pragma unroll
+        for (int c = 0; c < 16; c++) cs_[c][0] = L.cand[buf][c][0], cs_[c][1] = L.cand[buf][c][1];
+        sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+          if (cs_[c][0] < 0) continue;
+          const int k = (c >> 1) < 4 ? (c >> 1) : (c >> 1) + 1;
+          accept_sub(sel, frac_index(k % 3 - 1, k / 3 - 1), c & 1, cs_[c][0], cs_[c][1], thr);
         }
       }
-      BlockDesc d = make_desc(s, px, py, thr, true, 0);
-      int best_sad = s.sad;
+      stamp(a, mb, 4);
+      BlockDesc d = make_desc(sel, px, py, thr, true, 0);
+      int best_sad = sel.sad;
 
       // ---- classify_block (encode.cpp:17-67) ----
       if (a.inter) {
@@ -667,74 +787,95 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
           }
         }
       }
+      stamp(a, mb, 5);
 
-      // ---- prediction block (encode.cpp:80-141, decode.cpp:29-128) ----
+      // ---- per-wave 8x8 blocks: wave w owns blocks w and w+4 (w < 2) ----
+      // (encode_block encode.cpp:69-163, decode_block decode.cpp:15-144)
       const uint32_t type = d.block_type;
       const bool intra = (type & kIntra) != 0;
+      const bool has_pred = type != kIntra;
+      const bool intra_path = (type & kIntra) && !(type & kMotion);
       const PlaneSet pp =
           intra ? cs
                 : ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
                             (a.index + a.ring - d.prediction_target) % a.ring);
-      if (type != kIntra) {
-        const int mx = px + ((type & kMotion) ? d.motion_x : 0);
-        const int my = py + ((type & kMotion) ? d.motion_y : 0);
-        int dx = 0, dy = 0;
-        const bool sp = (type & kMotion) && d.sp_pred;
-        if (sp) frac_dir(d.sp_index, &dx, &dy);
-        for (int e = threadIdx.x; e < kMBElems; e += 256) {
-          int pl, ex, ey, nx, ny;
+      const int mx = px + ((type & kMotion) ? d.motion_x : 0);
+      const int my = py + ((type & kMotion) ? d.motion_y : 0);
+      int dx = 0, dy = 0;
+      const bool sp = (type & kMotion) && d.sp_pred;
+      if (sp) frac_dir(d.sp_index, &dx, &dy);
+      const int nblk = wave < 2 ? 2 : 1;
+      int pv[2] = {0, 0}, cf[2] = {0, 0};
+      for (int bi = 0; bi < nblk; bi++) {
+        const int b = wave + 4 * bi, e = b * 64 + lane;
+        int pl, ex, ey;
+        if (has_pred) {
           elem_coords(e, mx, my, pl, ex, ey);
           int v;
           if (intra) {
-            // from the staged window (identical bytes to the current slot)
-            const int16_t* t = pl == 0 ? L.win.y : (pl == 1 ? L.win.u : L.win.v);
-            const int pitch = pl == 0 ? kWinLP : kWinCP;
-            const int wx = pl == 0 ? ox : (ox >> 1), wy = pl == 0 ? oy : (oy >> 1);
-            v = t[(ey - wy) * pitch + ex - wx];
+            v = win_px(L.win, oy, pl, ex, ey);
             if (sp) {
+              int nx, ny;
               elem_coords(e, mx + dx, my + dy, pl, nx, ny);
-              v = lerp_px(v, t[(ny - wy) * pitch + nx - wx], d.sp_amount);
+              v = lerp_px(v, win_px(L.win, oy, pl, nx, ny), d.sp_amount);
             }
           } else {
-            const int16_t* t = pl == 0 ? pp.y : (pl == 1 ? pp.u : pp.v);
-            const int pitch = pl == 0 ? a.wa : (a.wa >> 1);
+            const int pitch = pl == 0 ? a.wa : cw;
+            const int16_t* t = plane_of(pp, pl);
             v = t[(size_t)ey * pitch + ex];
             if (sp) {
+              int nx, ny;
               elem_coords(e, mx + dx, my + dy, pl, nx, ny);
               v = lerp_px(v, t[(size_t)ny * pitch + nx], d.sp_amount);
             }
           }
-          L.pred[e] = (int16_t)v;
+          pv[bi] = v;
         }
-        __syncthreads();
+        if (type & kCopy) continue;
+        // residual (sub_8x8_line narrows to int16) -> forward transform
+        elem_coords(e, px, py, pl, ex, ey);
+        const int sv = plane_of(a.in, pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+        cf[bi] = fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
+                           has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
       }
-
-      // ---- encode_block + decode_block ----
-      if (type & kCopy) {
-        for (int e = threadIdx.x; e < kMBElems; e += 256) L.rec[e] = L.pred[e];
-        d.q_index = 0;
-        d.variance = 0;
-      } else {
+      stamp(a, mb, 6);
+      if (!(type & kCopy)) {
         int32_t v2;
-        uint32_t qp = code_mb(L.src, L.pred, type, a.quality, L.res, L.tmp, L.coef, L.qc, L.rec,
-                              L.red, &v2);
+        const int qp = vaq_mb(L.red, wave, lane, cf[0], a.quality, &v2);
         d.q_index = (uint8_t)qp;
         d.variance = (int16_t)v2;
-        for (int e = threadIdx.x; e < kMBElems; e += 256) {
+        for (int bi = 0; bi < nblk; bi++) {
+          const int b = wave + 4 * bi, e = b * 64 + lane;
+          const int16_t qv = quant_elem(e, cf[bi], qp, intra_path);
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
-          int16_t* p = pl == 0 ? a.coef.y : (pl == 1 ? a.coef.u : a.coef.v);
-          p[(size_t)ey * (pl ? a.wa >> 1 : a.wa) + ex] = L.qc[e];
+          int16_t* cp = pl == 0 ? a.coef.y : (pl == 1 ? a.coef.u : a.coef.v);
+          cp[(size_t)ey * (pl ? cw : a.wa) + ex] = qv;
+          const int t = idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
+                                  dequant_elem(e, qv, qp, intra_path));
+          pv[bi] = (int16_t)(has_pred ? t + pv[bi] : t);  // reconstruction (unclamped)
         }
+      } else {
+        d.q_index = 0;
+        d.variance = 0;
       }
-      for (int e = threadIdx.x; e < kMBElems; e += 256) {
+      stamp(a, mb, 7);
+      // reconstruction -> current slot (global) and the window
+      for (int bi = 0; bi < nblk; bi++) {
+        const int b = wave + 4 * bi, e = b * 64 + lane;
         int pl, ex, ey;
         elem_coords(e, px, py, pl, ex, ey);
         int16_t* p = pl == 0 ? cs.y : (pl == 1 ? cs.u : cs.v);
-        p[(size_t)ey * (pl ? a.wa >> 1 : a.wa) + ex] = L.rec[e];
+        p[(size_t)ey * (pl ? cw : a.wa) + ex] = (int16_t)pv[bi];
+        if (pl == 0)
+          L.win.y[(ey - oy) * kCwLP + (ex & 127)] = (int16_t)pv[bi];
+        else
+          (pl == 1 ? L.win.u : L.win.v)[(ey - (oy >> 1)) * kCwCP + (ex & 63)] = (int16_t)pv[bi];
       }
-      if (threadIdx.x == 0) a.table[mb] = d;
+      if (tid == 0) a.table[mb] = d;
+      stamp(a, mb, 8);
       publish(&done[by], bx + 1);
+      stamp(a, mb, 9);
     }
   }
 }
@@ -853,24 +994,32 @@ hipError_t launch_deblock(const FrameArgs& a, int workgroups, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_kat_transform(const int16_t* src, const int16_t* pred,
                                                        int16_t* coef, int16_t* recon,
                                                        const uint8_t* qtype, int32_t* qvar) {
-  __shared__ int16_t s_src[kMBElems], s_pred[kMBElems], res[kMBElems], tmp[kMBElems],
-      cf[kMBElems], qc[kMBElems], rec[kMBElems];
+  __shared__ alignas(16) int16_t sa[kMBElems], sb[kMBElems];
   __shared__ int32_t red[12];
-  const int m = blockIdx.x;
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    s_src[e] = src[m * kMBElems + e];
-    s_pred[e] = pred[m * kMBElems + e];
+  const int m = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t type = qtype[2 * m];
+  const int quality = qtype[2 * m + 1];
+  const bool has_pred = type != kIntra, intra_path = (type & kIntra) && !(type & kMotion);
+  const int nblk = wave < 2 ? 2 : 1;
+  int cf[2], pv[2];
+  for (int bi = 0; bi < nblk; bi++) {
+    const int e = (wave + 4 * bi) * 64 + lane;
+    pv[bi] = pred[m * kMBElems + e];
+    const int sv = src[m * kMBElems + e];
+    cf[bi] = fdct_lane(&sa[e - lane], &sb[e - lane], lane,
+                       has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
   }
-  __syncthreads();
   int32_t v2;
-  uint32_t q = code_mb(s_src, s_pred, qtype[2 * m], qtype[2 * m + 1], res, tmp, cf, qc, rec, red,
-                       &v2);
-  for (int e = threadIdx.x; e < kMBElems; e += 256) {
-    coef[m * kMBElems + e] = qc[e];
-    recon[m * kMBElems + e] = rec[e];
+  const int qp = vaq_mb(red, wave, lane, cf[0], quality, &v2);
+  for (int bi = 0; bi < nblk; bi++) {
+    const int e = (wave + 4 * bi) * 64 + lane;
+    const int16_t qv = quant_elem(e, cf[bi], qp, intra_path);
+    coef[m * kMBElems + e] = qv;
+    const int t = idct_lane(&sa[e - lane], &sb[e - lane], lane, dequant_elem(e, qv, qp, intra_path));
+    recon[m * kMBElems + e] = (int16_t)(has_pred ? t + pv[bi] : t);
   }
   if (threadIdx.x == 0) {
-    qvar[2 * m] = (int32_t)q;
+    qvar[2 * m] = qp;
     qvar[2 * m + 1] = v2;
   }
 }

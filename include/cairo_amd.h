@@ -74,8 +74,11 @@ CAIRO_API int cairo_ctx_read_planes(cairo_ctx *ctx, int which, int16_t *y, int16
 CAIRO_API int cairo_ctx_read_inter(cairo_ctx *ctx, uint8_t *descs, int32_t *sads);
 CAIRO_API int cairo_ctx_read_table(cairo_ctx *ctx, uint8_t *table);
 /* Debug: flags & 1 snapshots the reconstruction before the deblock of every
- * frame; cairo_ctx_read_predeblock returns the last snapshot. */
+ * frame (cairo_ctx_read_predeblock returns the last snapshot); flags & 2
+ * records per-macroblock phase timestamps of the wavefront kernel (10 x u64
+ * per MB, 100 MHz clock; cairo_ctx_read_stamps). */
 CAIRO_API int cairo_ctx_set_debug(cairo_ctx *ctx, int flags);
+CAIRO_API int cairo_ctx_read_stamps(cairo_ctx *ctx, uint64_t *out);
 CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, int16_t *v);
 
 /* Per-kernel timing (HIP events on the kernels' stream), opt-in. */
