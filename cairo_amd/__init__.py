@@ -244,7 +244,7 @@ class Context:
         return y, u, v
 
     def read_stamps(self) -> np.ndarray:
-        out = np.zeros((self.hmb, self.wmb, 10), np.uint64)
+        out = np.zeros((self.hmb, self.wmb, 12), np.uint64)
         _ck(self.L.cairo_ctx_read_stamps(self.h, _ptr(out)), "read_stamps")
         return out
 

@@ -62,6 +62,8 @@ struct cairo_ctx {
   bool have_inter = false;
   int16_t* predeblock = nullptr;  // debug snapshot of the slot after K2 (opt-in)
   uint64_t* stamps = nullptr;     // diagnostic K2 phase stamps (opt-in)
+  uint64_t* granules = nullptr;   // K2 macroblock hand-off granules
+  uint32_t epoch = 0;             // granule tag of the last submitted frame
 };
 
 namespace {
@@ -109,6 +111,7 @@ FrameArgs frame_args(const cairo_ctx* c, uint32_t index, uint32_t type, uint32_t
   a.sync = c->sync;
   a.sticky = c->sticky;
   a.stamps = c->stamps;
+  a.granules = c->granules;
   return a;
 }
 
@@ -137,6 +140,7 @@ void free_ctx(cairo_ctx* c) {
   (void)hipFree(c->rgb);
   (void)hipFree(c->predeblock);
   (void)hipFree(c->stamps);
+  (void)hipFree(c->granules);
   if (c->ks) (void)hipStreamDestroy(c->ks);
   if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
@@ -147,7 +151,11 @@ int zero_state(cairo_ctx* c) {
   CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2, c->ks));
   CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
   CK(hipMemsetAsync(c->table, 0, (size_t)c->wmb * c->hmb * sizeof(BlockDesc), c->ks));
+  // granule tags start at 0; the n-th submission after a reset publishes tag n.
+  CK(hipMemsetAsync(c->granules, 0, (size_t)c->wmb * c->hmb * kGranulesPerMB * sizeof(uint64_t),
+                    c->ks));
   CK(hipStreamSynchronize(c->ks));
+  c->epoch = 0;
   return kSuccess;
 }
 
@@ -198,6 +206,7 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   TRY(hipMalloc(&c->inter_sad, nref * mbs * sizeof(int32_t)));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t)));
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
+  TRY(hipMalloc(&c->granules, mbs * kGranulesPerMB * sizeof(uint64_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3));
   for (auto& s : c->st) {
@@ -291,6 +300,7 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
     if (r) return r;
   }
   FrameArgs a = frame_args(c, index, type, quality);
+  a.epoch = ++c->epoch;
   if (rgb_on_device) {
     a.rgb = rgb;
   } else {

@@ -19,7 +19,7 @@ constexpr int kMB = 16;               // EVX_MACROBLOCK_SIZE, macroblock.h:56
 constexpr int kSadGate = 8192;        // EVX_MOTION_SAD_THRESHOLD, motion.cpp:19
 constexpr int kRadius = 16;           // EVX_MOTION_SEARCH_RADIUS, motion.cpp:24
 constexpr int kQScale = 16;           // EVX_QUANTIZER_SCALE_FACTOR, quantize.cpp:9
-constexpr int kMaxRing = 8;           // ring sizes supported (reference: compile-time 4)
+constexpr int kMaxRing = 4;           // ring sizes 1..4 (reference: compile-time 4; R=5 is broken there)
 constexpr uint32_t kFeedCapacityBits = 32u * 1024u * 1024u;  // common.cpp:147
 
 // Block-type bits, types.h:68-87.

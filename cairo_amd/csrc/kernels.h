@@ -45,10 +45,19 @@ struct FrameArgs {
   int32_t* sync;           // SyncLayout words, zeroed before every frame
   int32_t* sticky;         // timeout flag that is never cleared (reported by the host)
   uint64_t* stamps;        // diagnostic: per-MB phase timestamps (nullptr = off)
+  uint64_t* granules;      // K2 hand-off: 192 {tag, 2 px} granules per macroblock
+  uint32_t epoch;          // granule tag of this frame (per-context submission count)
 };
 
+// Granule hand-off of a reconstructed macroblock (MI355X_MICROARCH.md, R2 form):
+// 8-byte {high: tag = FrameArgs::epoch, low: two int16 pixels}, each written by
+// ONE sc1 store; the reader polls the data itself.  Layout per macroblock:
+// 128 luma dwords (row r, pair d at r*8+d), then 32 U and 32 V (row r, pair d
+// at r*4+d).
+constexpr int kGranulesPerMB = 192;
+
 // Phase boundaries recorded per macroblock by k_mb_rows when stamps != nullptr.
-constexpr int kStampPhases = 10;
+constexpr int kStampPhases = 12;  // 10 real-time stamps + 2 shader-clock stamps
 
 // Words of FrameArgs::sync (all int32, zeroed per frame).
 struct SyncLayout {

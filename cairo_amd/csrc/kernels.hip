@@ -70,6 +70,10 @@ __device__ __forceinline__ int wave_max(int v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// A value every lane holds identically, moved to an SGPR so that the code
+// consuming it is scalar (no exec-mask divergence).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // Diagnostic timestamp (100 MHz constant clock) of phase k of macroblock mb.
 __device__ __forceinline__ void stamp(const FrameArgs& a, int mb, int k) {
   if (a.stamps && threadIdx.x == 0)
@@ -114,6 +118,36 @@ __device__ __forceinline__ void publish(int32_t* word, int value) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Granule hand-off (kernels.h kGranulesPerMB): one 8-byte sc1 store per
+// granule on the producer, sc1 loads on the consumer, the tag is the flag.
+// Global address space so the compiler emits global_ (never flat_) accesses.
+typedef __attribute__((address_space(1))) uint64_t gbl_u64;
+__device__ __forceinline__ uint64_t gran_ld(const uint64_t* p) {
+  return __hip_atomic_load((const gbl_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gran_st(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((gbl_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Data of granule p, given a first load g: re-polls until the tag matches.
+// Bounded like wait_at_least (the error word ends every other wait too).
+__device__ __forceinline__ uint32_t gran_settle(const uint64_t* p, uint64_t g, uint32_t tag,
+                                                int32_t* err, int32_t* sticky) {
+  if ((uint32_t)(g >> 32) == tag) return (uint32_t)g;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    __builtin_amdgcn_s_sleep(1);
+    g = gran_ld(p);
+    if ((uint32_t)(g >> 32) == tag) break;
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  return (uint32_t)g;
 }
 
 // Dequeue the next task index for this workgroup (uniform result).
@@ -293,6 +327,92 @@ __device__ __forceinline__ void accept_sub(Sel& s, int idx, int quarter, int sad
     s.sp_idx = idx;
     s.sad = sad;
     s.mad = mad;
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Parallel replay of the reference's sequential candidate acceptance.
+//
+// Lanes 0..15 of a wave hold candidates in scan order (index c = lane).  The
+// fold of evaluate_motion_candidate (motion.cpp:111-149) over a step is:
+//  * copy mode (best_mad < thr): keep the lexicographic minimum of
+//    (mad, ssd), earlier wins exact ties;
+//  * otherwise the first candidate with mad < thr is taken unconditionally and
+//    switches to copy mode; without one, the minimum of (sad, ssd gated by
+//    sad < 8192), earlier wins ties.
+// evaluate_subpel_motion_candidate (motion.cpp:151-223) is the same with keys
+// (mad) and (sad, only if sad < 8192).  Keys carry the index, so every key is
+// unique and min() picks exactly the candidate the sequential loop ends on.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t row0_min(uint32_t v) {  // min over lanes 0..15
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xF, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+}
+
+__device__ __forceinline__ uint32_t key_copy(int mad, int ssd, int idx) {
+  return ((uint32_t)min(mad, 65535) << 16) | ((uint32_t)min(ssd, 4095) << 4) | (uint32_t)idx;
+}
+__device__ __forceinline__ uint32_t key_sad(int sad, int ssd, int idx) {
+  if (sad < kSadGate)
+    return ((uint32_t)sad << 18) | ((uint32_t)min(ssd, 16383) << 4) | (uint32_t)idx;
+  return 0x80000000u | ((uint32_t)min(sad, (1 << 27) - 1) << 4) | (uint32_t)idx;
+}
+
+// Integer step: this lane's candidate (valid, cx, cy, sad, mad); c = lane & 15.
+__device__ __forceinline__ void select_int(Sel& s, bool valid, int cx, int cy, int sad, int mad,
+                                           int px, int py, int thr, int lane) {
+  const int c = lane & 15;
+  const bool live = lane < 16 && valid;
+  const int ssd = (cx - px) * (cx - px) + (cy - py) * (cy - py);
+  const uint32_t fm = (uint32_t)__ballot(live && mad < thr);
+  int w = -1;  // winning candidate, -1 = keep the state
+  if (s.mad < thr || fm) {
+    const int f = s.mad < thr ? -1 : (int)__builtin_ctz(fm);
+    const uint32_t k = row0_min(live && c >= f ? key_copy(mad, ssd, c + 1) : 0xFFFFFFFFu);
+    if (f >= 0) w = (int)(k & 15) - 1;  // candidate f is always in the running
+    else if (k < key_copy(s.mad, s.ssd, 0)) w = (int)(k & 15) - 1;
+  } else {
+    const uint32_t k = row0_min(live ? key_sad(sad, ssd, c + 1) : 0xFFFFFFFFu);
+    if (k < key_sad(s.sad, s.ssd, 0)) w = (int)(k & 15) - 1;
+  }
+  if (w >= 0) {
+    s.bx = __builtin_amdgcn_readlane(cx, w);
+    s.by = __builtin_amdgcn_readlane(cy, w);
+    s.sad = __builtin_amdgcn_readlane(sad, w);
+    s.ssd = __builtin_amdgcn_readlane(ssd, w);
+    s.mad = __builtin_amdgcn_readlane(mad, w);
+  }
+}
+
+// Sub-pel step: candidate c = 2*n + q (neighbour n, q = quarter).
+__device__ __forceinline__ void select_sub(Sel& s, bool valid, int sad, int mad, int thr, int lane) {
+  const int c = lane & 15;
+  const bool live = lane < 16 && valid;
+  const uint32_t fm = (uint32_t)__ballot(live && mad < thr);
+  int w = -1;
+  if (s.mad < thr || fm) {
+    const int f = s.mad < thr ? -1 : (int)__builtin_ctz(fm);
+    const uint32_t k = row0_min(live && c >= f ? (((uint32_t)min(mad, 65535) << 5) | (uint32_t)(c + 1))
+                                               : 0xFFFFFFFFu);
+    if (f >= 0) w = (int)(k & 31) - 1;
+    else if (k < ((uint32_t)min(s.mad, 65535) << 5)) w = (int)(k & 31) - 1;
+  } else {
+    const uint32_t k =
+        row0_min(live && sad < kSadGate ? (((uint32_t)sad << 5) | (uint32_t)(c + 1)) : 0xFFFFFFFFu);
+    if (k < ((uint32_t)min(s.sad, 1 << 26) << 5)) w = (int)(k & 31) - 1;
+  }
+  if (w >= 0) {
+    const int n = w >> 1, k9 = n < 4 ? n : n + 1;
+    s.sp_en = 1;
+    s.sp_amt = w & 1;
+    s.sp_idx = frac_index(k9 % 3 - 1, k9 / 3 - 1);
+    s.sad = __builtin_amdgcn_readlane(sad, w);
+    s.mad = __builtin_amdgcn_readlane(mad, w);
   }
 }
 
@@ -514,9 +634,12 @@ __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool i
 //
 // The current slot around the row lives in a circular LDS window: MB rows
 // by-3..by+1 (80 pixel rows) by 128 columns addressed with absolute x & 127.
-// A step loads only the new column (rows by-3..by-1 at bx+2) and one stale
+// A step brings in only the new column (rows by-3..by-1 at bx+2) and one stale
 // macroblock (row by+1 at bx-1); the row's own reconstruction is written
-// straight into the window.
+// straight into the window.  Finished macroblocks are handed to the rows
+// below as tagged granules (no flag, no fence: MI355X_MICROARCH.md R2), and
+// "row by-1 finished bx+2" is simply "granules of (bx+2, by-1) carry this
+// frame's tag".
 // ---------------------------------------------------------------------------
 
 constexpr int kCwLP = 130;  // luma window pitch (elements): 128 columns, odd dword stride
@@ -536,32 +659,22 @@ struct alignas(16) RowLds {
   int slot;
 };
 
-// Move dword k (0..191) of macroblock (mbx, mby) of plane set p into the window.
-__device__ __forceinline__ void win_put(RowWindow& w, const PlaneSet& p, int wa, int oy, int mbx,
-                                        int mby, int k) {
+// Dword k (0..191) of macroblock (mbx, mby): its address in plane set p and in
+// the window (same order as the granules, kernels.h).
+__device__ __forceinline__ const int16_t* win_src(const PlaneSet& p, int wa, int mbx, int mby, int k) {
+  if (k < 128) return p.y + (size_t)(mby * 16 + (k >> 3)) * wa + mbx * 16 + 2 * (k & 7);
+  const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
+  return (pl ? p.v : p.u) + (size_t)(mby * 8 + r) * (wa >> 1) + mbx * 8 + 2 * d;
+}
+__device__ __forceinline__ uint32_t* win_dst(RowWindow& w, int oy, int mbx, int mby, int k) {
   if (k < 128) {
-    const int r = k >> 3, d = k & 7;
-    const int gy = mby * 16 + r, gx = mbx * 16 + 2 * d;
-    const uint32_t v = *(const uint32_t*)(p.y + (size_t)gy * wa + gx);
-    *(uint32_t*)&w.y[(gy - oy) * kCwLP + (gx & 127)] = v;
-  } else {
-    const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
-    const int gy = mby * 8 + r, gx = mbx * 8 + 2 * d;
-    const int16_t* s = (pl ? p.v : p.u) + (size_t)gy * (wa >> 1) + gx;
-    int16_t* dst = pl ? w.v : w.u;
-    *(uint32_t*)&dst[(gy - (oy >> 1)) * kCwCP + (gx & 63)] = *(const uint32_t*)s;
+    const int gy = mby * 16 + (k >> 3), gx = mbx * 16 + 2 * (k & 7);
+    return (uint32_t*)&w.y[(gy - oy) * kCwLP + (gx & 127)];
   }
+  const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
+  const int gy = mby * 8 + r, gx = mbx * 8 + 2 * d;
+  return (uint32_t*)&(pl ? w.v : w.u)[(gy - (oy >> 1)) * kCwCP + (gx & 63)];
 }
-
-// Load a list of macroblocks (n <= 9) into the window; all threads.
-__device__ __forceinline__ void win_load(RowWindow& w, const PlaneSet& p, int wa, int oy,
-                                         const int* mbx, const int* mby, int n) {
-  for (int k = threadIdx.x; k < n * 192; k += 256) {
-    const int i = k / 192;
-    win_put(w, p, wa, oy, mbx[i], mby[i], k - i * 192);
-  }
-}
-
 // Sum / max over one 16-lane DPP row (a candidate's group); all 16 lanes get it.
 __device__ __forceinline__ int row16_sum(int v) {
   v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
@@ -648,6 +761,42 @@ __device__ __forceinline__ const int16_t* plane_of(const PlaneSet& p, int pl) {
   return pl == 0 ? p.y : (pl == 1 ? p.u : p.v);
 }
 
+// Prediction sample of element e (block-major) of the block at (mx, my) of
+// plane set p, lerped toward (mx+dx, my+dy) when sp (macroblock.h:203-259).
+__device__ __forceinline__ int pred_global(const PlaneSet& p, int wa, int e, int mx, int my, bool sp,
+                                           int dx, int dy, int amount) {
+  int pl, ex, ey;
+  elem_coords(e, mx, my, pl, ex, ey);
+  const int pitch = pl == 0 ? wa : (wa >> 1);
+  const int16_t* t = plane_of(p, pl);
+  int v = t[(size_t)ey * pitch + ex];
+  if (sp) {
+    int nx, ny;
+    elem_coords(e, mx + dx, my + dy, pl, nx, ny);
+    v = lerp_px(v, t[(size_t)ny * pitch + nx], amount);
+  }
+  return v;
+}
+
+__device__ __forceinline__ BlockDesc uni_desc(const BlockDesc& d) {
+  BlockDesc u;
+  u.block_type = (uint32_t)uni((int)d.block_type);
+  u.prediction_target = (uint8_t)uni(d.prediction_target);
+  u.pad = 0;
+  u.motion_x = (int16_t)uni(d.motion_x);
+  u.motion_y = (int16_t)uni(d.motion_y);
+  u.sp_pred = (uint8_t)uni(d.sp_pred);
+  u.sp_amount = (uint8_t)uni(d.sp_amount);
+  u.sp_index = (uint8_t)uni(d.sp_index);
+  u.q_index = 0;
+  u.variance = 0;
+  return u;
+}
+
+__device__ __forceinline__ uint64_t* gran_at(const FrameArgs& a, int mbx, int mby, int k) {
+  return a.granules + (size_t)(mby * a.wmb + mbx) * kGranulesPerMB + k;
+}
+
 __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
   __shared__ RowLds L;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -655,8 +804,10 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
   const int thr = (a.quality >> 2) + 1;
   const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
   int32_t* err = a.sync + SyncLayout::kErr;
-  int32_t* done = a.sync + SyncLayout::kRowDone;
+  const uint32_t tag = a.epoch;
   const int cw = a.wa >> 1;
+  const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
+  const int mbs = a.wmb * a.hmb;
 
   for (;;) {
     const int by = dequeue(a.sync + SyncLayout::kRowTicket, &L.slot);
@@ -665,27 +816,30 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
       stamp(a, mb, 0);
-      // ---- window maintenance ----
-      int lx[9], ly[9], n = 0;
-      if (bx > 0) {  // older rows of the new column, and the stale block of row by+1
-        for (int r = by - 3; r <= by - 2; r++)
-          if (r >= 0 && bx + 2 < a.wmb) lx[n] = bx + 2, ly[n++] = r;
-        if (by + 1 < a.hmb) lx[n] = bx - 1, ly[n++] = by + 1;
-        win_load(L.win, cs, a.wa, oy, lx, ly, n);
-        n = 0;
-      }
+      if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
+
+      // ---- window.  Reconstruction of the rows above arrives as granules
+      //      (this frame's data, polled by tag); the stale row below is the
+      //      previous launch's slot.  Immediate: the fresh column block
+      //      (bx+2, by-1), or at bx == 0 the first three columns.  Prefetched
+      //      for MB bx+1 and committed at the end of this macroblock: column
+      //      bx+3 of rows by-3, by-2 (final once row by-1 passed bx+2) and the
+      //      stale block (bx, by+1), read before row by+1 may rewrite it ----
       if (by > 0) {
-        if (tid == 0) wait_at_least(&done[by - 1], min(bx + 3, a.wmb), err, a.sticky);
-        acquire_after_wait();
         if (bx == 0) {
+          int lx[9], ly[9], n = 0;
           for (int r = max(by - 3, 0); r <= by - 1; r++)
             for (int c = 0; c <= 2 && c < a.wmb; c++) lx[n] = c, ly[n++] = r;
-        } else if (bx + 2 < a.wmb) {
-          lx[n] = bx + 2, ly[n++] = by - 1;
+          for (int k = tid; k < n * kGranulesPerMB; k += 256) {
+            const int i = k / kGranulesPerMB, kk = k - i * kGranulesPerMB;
+            const uint64_t* gp = gran_at(a, lx[i], ly[i], kk);
+            *win_dst(L.win, oy, lx[i], ly[i], kk) = gran_settle(gp, gran_ld(gp), tag, err, a.sticky);
+          }
+        } else if (bx + 2 < a.wmb && tid < kGranulesPerMB) {
+          const uint64_t* gp = gran_at(a, bx + 2, by - 1, tid);
+          *win_dst(L.win, oy, bx + 2, by - 1, tid) = gran_settle(gp, gran_ld(gp), tag, err, a.sticky);
         }
-        win_load(L.win, cs, a.wa, oy, lx, ly, n);
       }
-      stamp(a, mb, 1);
       // source rows of this lane's group slot
       SrcRow s;
       {
@@ -698,6 +852,37 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
         s.u[0] = u4.x, s.u[1] = u4.y, s.u[2] = u4.z, s.u[3] = u4.w;
         s.v[0] = v4.x, s.v[1] = v4.y, s.v[2] = v4.z, s.v[3] = v4.w;
       }
+      const bool pf3 = by >= 3 && bx + 3 < a.wmb, pf2 = by >= 2 && bx + 3 < a.wmb;
+      const bool pfs = by + 1 < a.hmb && bx + 1 < a.wmb;
+      uint64_t pg3 = 0, pg2 = 0;
+      uint32_t pst = 0;
+      if (tid < kGranulesPerMB) {
+        if (pf3) pg3 = gran_ld(gran_at(a, bx + 3, by - 3, tid));
+        if (pf2) pg2 = gran_ld(gran_at(a, bx + 3, by - 2, tid));
+        if (pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);
+      }
+
+      // ---- inter predictions, prefetched (the K1 records are final) ----
+      BlockDesc inter_d[kMaxRing - 1];
+      int inter_sad[kMaxRing - 1];
+      int ipv[kMaxRing - 1][2];
+      const int nref = a.inter ? a.ring - 1 : 0;
+#pragma unroll
+      for (int o = 0; o < kMaxRing - 1; o++) {
+        if (o >= nref) break;
+        inter_d[o] = uni_desc(a.inter_desc[o * mbs + mb]);
+        inter_sad[o] = uni(a.inter_sad[o * mbs + mb]);
+        const BlockDesc& d = inter_d[o];
+        const PlaneSet rp = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
+                                      (a.index + a.ring - d.prediction_target) % a.ring);
+        const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
+        int dx = 0, dy = 0;
+        if (sp) frac_dir(d.sp_index, &dx, &dy);
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
+          ipv[o][bi] = pred_global(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
+                                   py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
+      }
+      stamp(a, mb, 1);
       __syncthreads();
       stamp(a, mb, 2);
 
@@ -707,7 +892,7 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
         int sm = 0;
 #pragma unroll
         for (int k = 0; k < 16; k++) sm += abs(s.y[k]);
-        sel.sad = row16_sum(sm);  // compute_block_sad(src): every group holds the total
+        sel.sad = uni(row16_sum(sm));  // compute_block_sad(src): every group holds the total
       }
       sel.bx = px;
       sel.by = py;
@@ -715,28 +900,28 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
       sel.ssd = INT32_MAX;
       sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
       int buf = 0;
+#pragma unroll 1
       for (int stage = 0; stage < 5; stage++) {
         const int step = stage == 0 ? kRadius : (kRadius >> stage);
         const int jlo = stage == 0 ? -2 * kRadius : -step;
         const int bx0 = sel.bx, by0 = sel.by;
-        if (grp < 9) {
-          const int cx = bx0 - step + (grp % 3) * step, cy = by0 + jlo + (grp / 3) * step;
-          int sad = -1, mad = -1;
-          if (intra_valid(cx, cy, px, py, a.wa, a.ha)) cand_row(L.win, oy, cx, cy, gi, s, sad, mad);
-          if (gi == 0) {
-            L.cand[buf][grp][0] = sad;
+        {  // group g < 9 evaluates candidate g; groups 9..15 repeat candidate 8
+          const int c = min(grp, 8);
+          const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
+          const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
+          int sad, mad;
+          cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
+          if (gi == 0 && grp < 9) {
+            L.cand[buf][grp][0] = ok ? sad : -1;
             L.cand[buf][grp][1] = mad;
           }
         }
         __syncthreads();
-        int cs_[9][2];
-#pragma unroll
-        for (int c = 0; c < 9; c++) cs_[c][0] = L.cand[buf][c][0], cs_[c][1] = L.cand[buf][c][1];
-#pragma unroll
-        for (int c = 0; c < 9; c++) {
-          if (cs_[c][0] < 0) continue;
+        {
+          const int c = lane & 15;
+          const int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
           const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
-          accept_int(sel, cx, cy, cs_[c][0], cs_[c][1], px, py, thr);
+          select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
         }
         buf ^= 1;
       }
@@ -746,97 +931,75 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
         const int nn = grp >> 1, q = grp & 1;
         const int k9 = nn < 4 ? nn : nn + 1;  // skip the centre of the 3x3
         const int tx = bx0 + k9 % 3 - 1, ty = by0 + k9 / 3 - 1;
-        int sad = -1, mad = -1;
-        if (intra_valid(tx, ty, px, py, a.wa, a.ha))
-          subpel_row(L.win, oy, bx0, by0, tx, ty, q, gi, s, sad, mad);
+        const bool ok = intra_valid(tx, ty, px, py, a.wa, a.ha);
+        int sad, mad;
+        subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, q, gi, s, sad, mad);
         if (gi == 0) {
-          L.cand[buf][grp][0] = sad;
+          L.cand[buf][grp][0] = ok ? sad : -1;
           L.cand[buf][grp][1] = mad;
         }
         __syncthreads();
-        int cs_[16][2];
-#pragma unroll
-        for (int c = 0; c < 16; c++) cs_[c][0] = L.cand[buf][c][0], cs_[c][1] = L.cand[buf][c][1];
+        const int vs = L.cand[buf][lane & 15][0], vm = L.cand[buf][lane & 15][1];
         sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-          if (cs_[c][0] < 0) continue;
-          const int k = (c >> 1) < 4 ? (c >> 1) : (c >> 1) + 1;
-          accept_sub(sel, frac_index(k % 3 - 1, k / 3 - 1), c & 1, cs_[c][0], cs_[c][1], thr);
-        }
+        select_sub(sel, vs >= 0, vs, vm, thr, lane);
       }
       stamp(a, mb, 4);
       BlockDesc d = make_desc(sel, px, py, thr, true, 0);
       int best_sad = sel.sad;
+      bool from_inter = false;  // an inter record won (its prediction is in wpv)
+      int wpv[2] = {0, 0};
 
       // ---- classify_block (encode.cpp:17-67) ----
-      if (a.inter) {
-        const int mbs = a.wmb * a.hmb;
-        for (int off = 1; off < a.ring; off++) {
-          const BlockDesc in = a.inter_desc[(off - 1) * mbs + mb];
-          const int isad = a.inter_sad[(off - 1) * mbs + mb];
-          const bool ci = (in.block_type & kCopy) != 0, cb = (d.block_type & kCopy) != 0;
-          if (ci != cb) {
-            if (ci) {
-              d = in;
-              best_sad = isad;
-            }
-          } else if (isad < best_sad) {
-            d = in;
-            best_sad = isad;
-          }
+#pragma unroll
+      for (int o = 0; o < kMaxRing - 1; o++) {
+        if (o >= nref) break;
+        const bool ci = (inter_d[o].block_type & kCopy) != 0, cb = (d.block_type & kCopy) != 0;
+        if (ci != cb ? ci : inter_sad[o] < best_sad) {
+          d = inter_d[o];
+          best_sad = inter_sad[o];
+          from_inter = true;
+          wpv[0] = ipv[o][0];
+          wpv[1] = ipv[o][1];
         }
       }
       stamp(a, mb, 5);
 
-      // ---- per-wave 8x8 blocks: wave w owns blocks w and w+4 (w < 2) ----
-      // (encode_block encode.cpp:69-163, decode_block decode.cpp:15-144)
+      // ---- per-wave 8x8 blocks (encode_block encode.cpp:69-163,
+      //      decode_block decode.cpp:15-144) ----
       const uint32_t type = d.block_type;
-      const bool intra = (type & kIntra) != 0;
       const bool has_pred = type != kIntra;
       const bool intra_path = (type & kIntra) && !(type & kMotion);
-      const PlaneSet pp =
-          intra ? cs
-                : ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
-                            (a.index + a.ring - d.prediction_target) % a.ring);
-      const int mx = px + ((type & kMotion) ? d.motion_x : 0);
-      const int my = py + ((type & kMotion) ? d.motion_y : 0);
-      int dx = 0, dy = 0;
-      const bool sp = (type & kMotion) && d.sp_pred;
-      if (sp) frac_dir(d.sp_index, &dx, &dy);
-      const int nblk = wave < 2 ? 2 : 1;
       int pv[2] = {0, 0}, cf[2] = {0, 0};
-      for (int bi = 0; bi < nblk; bi++) {
-        const int b = wave + 4 * bi, e = b * 64 + lane;
-        int pl, ex, ey;
-        if (has_pred) {
+      if (from_inter) {
+        pv[0] = wpv[0];
+        pv[1] = wpv[1];
+      } else if (has_pred) {  // intra motion: prediction from the window
+        const int mx = px + d.motion_x, my = py + d.motion_y;
+        const bool sp = d.sp_pred;
+        int dx = 0, dy = 0;
+        if (sp) frac_dir(d.sp_index, &dx, &dy);
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+          const int e = (wave + 4 * bi) * 64 + lane;
+          int pl, ex, ey;
           elem_coords(e, mx, my, pl, ex, ey);
-          int v;
-          if (intra) {
-            v = win_px(L.win, oy, pl, ex, ey);
-            if (sp) {
-              int nx, ny;
-              elem_coords(e, mx + dx, my + dy, pl, nx, ny);
-              v = lerp_px(v, win_px(L.win, oy, pl, nx, ny), d.sp_amount);
-            }
-          } else {
-            const int pitch = pl == 0 ? a.wa : cw;
-            const int16_t* t = plane_of(pp, pl);
-            v = t[(size_t)ey * pitch + ex];
-            if (sp) {
-              int nx, ny;
-              elem_coords(e, mx + dx, my + dy, pl, nx, ny);
-              v = lerp_px(v, t[(size_t)ny * pitch + nx], d.sp_amount);
-            }
+          int v = win_px(L.win, oy, pl, ex, ey);
+          if (sp) {
+            int nx, ny;
+            elem_coords(e, mx + dx, my + dy, pl, nx, ny);
+            v = lerp_px(v, win_px(L.win, oy, pl, nx, ny), d.sp_amount);
           }
           pv[bi] = v;
         }
-        if (type & kCopy) continue;
-        // residual (sub_8x8_line narrows to int16) -> forward transform
-        elem_coords(e, px, py, pl, ex, ey);
-        const int sv = plane_of(a.in, pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
-        cf[bi] = fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
-                           has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
+      }
+      if (!(type & kCopy)) {
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {  // residual (int16) -> forward transform
+          const int b = wave + 4 * bi, e = b * 64 + lane;
+          int pl, ex, ey;
+          elem_coords(e, px, py, pl, ex, ey);
+          const int sv = plane_of(a.in, pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+          cf[bi] = fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
+                             has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
+        }
       }
       stamp(a, mb, 6);
       if (!(type & kCopy)) {
@@ -844,7 +1007,7 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
         const int qp = vaq_mb(L.red, wave, lane, cf[0], a.quality, &v2);
         d.q_index = (uint8_t)qp;
         d.variance = (int16_t)v2;
-        for (int bi = 0; bi < nblk; bi++) {
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
           const int b = wave + 4 * bi, e = b * 64 + lane;
           const int16_t qv = quant_elem(e, cf[bi], qp, intra_path);
           int pl, ex, ey;
@@ -861,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
       }
       stamp(a, mb, 7);
       // reconstruction -> current slot (global) and the window
-      for (int bi = 0; bi < nblk; bi++) {
+      _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
         const int b = wave + 4 * bi, e = b * 64 + lane;
         int pl, ex, ey;
         elem_coords(e, px, py, pl, ex, ey);
@@ -872,10 +1035,30 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
         else
           (pl == 1 ? L.win.u : L.win.v)[(ey - (oy >> 1)) * kCwCP + (ex & 63)] = (int16_t)pv[bi];
       }
+      if (tid < kGranulesPerMB) {  // prefetched window blocks for MB bx+1
+        if (pf3)
+          *win_dst(L.win, oy, bx + 3, by - 3, tid) =
+              gran_settle(gran_at(a, bx + 3, by - 3, tid), pg3, tag, err, a.sticky);
+        if (pf2)
+          *win_dst(L.win, oy, bx + 3, by - 2, tid) =
+              gran_settle(gran_at(a, bx + 3, by - 2, tid), pg2, tag, err, a.sticky);
+        if (pfs) *win_dst(L.win, oy, bx, by + 1, tid) = pst;
+      }
       if (tid == 0) a.table[mb] = d;
       stamp(a, mb, 8);
-      publish(&done[by], bx + 1);
+      // publish: pixel pairs (lane, lane^1) of each 8x8 block as granules
+      _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+        const int b = wave + 4 * bi;
+        const int nb = __builtin_amdgcn_mov_dpp(pv[bi], 0xB1, 0xF, 0xF, false);  // lane ^ 1
+        if (!(lane & 1)) {
+          const int r = lane >> 3, c2 = (lane & 7) >> 1;
+          const int k = b < 4 ? (((b >> 1) * 8 + r) * 8 + (b & 1) * 4 + c2) : (128 + (b - 4) * 32 + r * 4 + c2);
+          gran_st(gran_at(a, bx, by, k),
+                  ((uint64_t)tag << 32) | ((uint32_t)pv[bi] & 0xFFFFu) | ((uint32_t)nb << 16));
+        }
+      }
       stamp(a, mb, 9);
+      if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
   }
 }

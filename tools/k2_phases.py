@@ -28,7 +28,7 @@ for t in range(a.frames):
     ctx.encode_frame(cairo_amd.make_band4(w, h, t), t, t > 0, q)
     ctx.sync()
 st = ctx.read_stamps().astype(np.int64)  # (hmb, wmb, 10), 10 ns ticks
-d = np.diff(st, axis=2) / 100.0  # us
+d = np.diff(st[..., :10], axis=2) / 100.0  # us
 print(f"{a.config} frame {a.frames - 1}: per-MB phase means (us) over {st.shape[0] * st.shape[1]} MBs")
 for k, name in enumerate(PHASES):
     print(f"  {name:11s} mean {d[..., k].mean():8.3f}  p50 {np.median(d[..., k]):8.3f}  max {d[..., k].max():8.3f}")
@@ -43,5 +43,7 @@ for by in range(1, hb):
         lat.append((st[by, bx, 1] - st[by - 1, src, 9]) / 100.0)
 lat = np.array(lat)
 print(f"  hand-off (publish -> resume) mean {lat.mean():.3f} p50 {np.median(lat):.3f} us")
+clk = (st[..., 11] - st[..., 10]) / np.maximum(st[..., 9] - st[..., 0], 1) * 100.0  # MHz
+print(f"  effective shader clock: mean {clk.mean():.0f} MHz, p10 {np.percentile(clk, 10):.0f}, p90 {np.percentile(clk, 90):.0f}")
 span = (st[..., 9].max() - st[..., 0].min()) / 100.0
 print(f"  kernel span {span:.1f} us, steps {wb + 3 * (hb - 1)}, per step {span / (wb + 3 * (hb - 1)):.3f} us")
