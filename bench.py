@@ -66,6 +66,23 @@ def algorithmic_bytes(w, h, ring):
     }
 
 
+def max_over_ranks(x: float, dist, device) -> float:
+    """Max of a per-rank float over the process group (identity without one).
+    device: where the collective's tensor lives (cuda for nccl, cpu for gloo)."""
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_mpix(w: int, h: int, steps: int, world: int, elapsed_max: float) -> float:
+    """Whole-job throughput: every rank encodes `steps` frames of w x h (weak scaling)."""
+    return w * h * steps * world / elapsed_max / 1e6
+
+
 def run_hot_path(ctx, dev_frames, frame_ptr, first, count, quality, stages, entropy=None):
     """Submit frames [first, first+count) with up to `stages` in flight."""
     inflight = deque()
@@ -137,13 +154,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms, kframes = ctx.take_timings()
     ctx.set_profiling(False)
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    pixels = w * h * a.steps * world
-    value = pixels / elapsed / 1e6
+    elapsed = max_over_ranks(elapsed, dist, dev)
+    value = aggregate_mpix(w, h, a.steps, world, elapsed)
     per_kernel = {k: kernel_ms[i] / max(kframes, 1) for i, k in enumerate(["convert", "inter_search", "mb_rows", "deblock"])}
     abytes = algorithmic_bytes(w, h, ring)
     dominant = max(per_kernel, key=per_kernel.get)
@@ -238,13 +250,8 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, 
     barrier()
     el = time.perf_counter() - t0
     pool.shutdown(wait=True)
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    return {"value": round(w * h * a.steps * world / el / 1e6, 3), "unit": "Mpix/s",
+    el = max_over_ranks(el, dist, dev)
+    return {"value": round(aggregate_mpix(w, h, a.steps, world, el), 3), "unit": "Mpix/s",
             "ms_per_step": round(el * 1e3 / a.steps, 4), "entropy_threads": a.entropy_threads,
             "staging_slots": stages,
             "note": "hot path + host entropy (serialize_slice) pipelined; bitstreams produced"}

@@ -47,7 +47,7 @@ typedef struct cairo_frame_result {
 /* Context = one encoder's device state: R ring slots, input and output_cache
  * planes, block table, inter-search records, staging.  width/height are the
  * nominal frame size (aligned up to 16 internally, evx1enc.cpp:79-80); ring is
- * R = EVX_REFERENCE_FRAME_COUNT (2..8); device is the HIP ordinal. */
+ * R = EVX_REFERENCE_FRAME_COUNT (1..4); device is the HIP ordinal. */
 CAIRO_API int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
                                cairo_ctx **out);
 CAIRO_API int cairo_ctx_destroy(cairo_ctx *ctx);
@@ -75,7 +75,7 @@ CAIRO_API int cairo_ctx_read_inter(cairo_ctx *ctx, uint8_t *descs, int32_t *sads
 CAIRO_API int cairo_ctx_read_table(cairo_ctx *ctx, uint8_t *table);
 /* Debug: flags & 1 snapshots the reconstruction before the deblock of every
  * frame (cairo_ctx_read_predeblock returns the last snapshot); flags & 2
- * records per-macroblock phase timestamps of the wavefront kernel (10 x u64
+ * records per-macroblock phase timestamps of the wavefront kernel (12 x u64
  * per MB, 100 MHz clock; cairo_ctx_read_stamps). */
 CAIRO_API int cairo_ctx_set_debug(cairo_ctx *ctx, int flags);
 CAIRO_API int cairo_ctx_read_stamps(cairo_ctx *ctx, uint64_t *out);
