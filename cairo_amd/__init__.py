@@ -1,7 +1,7 @@
 """cairo_amd -- MI355X-native EVX-1 (hinike/cairo) encode path.
 
 The product is ``_lib/libcairo_amd.so``: hand-written HIP kernels for gfx950
-(convert, inter search, macroblock wavefront, deblock), the host entropy stage
+(convert, inter search, macroblock wavefront with in-loop deblock), the host entropy stage
 and the drop-in ``evx1_encoder`` / ``bit_stream`` C++ API.  This module is a
 thin ctypes view of its C ABI (``include/cairo_amd.h``) for tests, the bench
 and Python callers.  There is no Python or CPU fallback for the hot path: if
@@ -76,7 +76,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_read_stamps": (I, [P, P]),
         "cairo_ctx_set_profiling": (I, [P, I]),
         "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
-        "cairo_ctx_set_workgroups": (I, [P, I, I]),
+        "cairo_ctx_set_workgroups": (I, [P, I]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "evx_encoder_create": (I, [ctypes.POINTER(P)]),
@@ -243,22 +243,26 @@ class Context:
         _ck(self.L.cairo_ctx_read_predeblock(self.h, _ptr(y), _ptr(u), _ptr(v)), "read_predeblock")
         return y, u, v
 
-    def read_stamps(self) -> np.ndarray:
-        out = np.zeros((self.hmb, self.wmb, 12), np.uint64)
+    def read_stamps(self):
+        """-> (per-MB stamps (hmb, wmb, 12), per-row deblock stamps (hmb, 9),
+        kernel [entry, exit]); 100 MHz ticks."""
+        n_mb, n_db = self.hmb * self.wmb * 12, self.hmb * 9
+        out = np.zeros(n_mb + n_db + 2, np.uint64)
         _ck(self.L.cairo_ctx_read_stamps(self.h, _ptr(out)), "read_stamps")
-        return out
+        return (out[:n_mb].reshape(self.hmb, self.wmb, 12), out[n_mb:n_mb + n_db].reshape(self.hmb, 9),
+                out[n_mb + n_db:])
 
     def set_profiling(self, enable: bool) -> None:
         _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")
 
     def take_timings(self):
-        ms = (ctypes.c_double * 4)()
+        ms = (ctypes.c_double * 3)()
         n = ctypes.c_int()
         _ck(self.L.cairo_ctx_take_timings(self.h, ms, ctypes.byref(n)), "take_timings")
         return list(ms), n.value
 
-    def set_workgroups(self, rows: int = 0, deblock: int = 0) -> None:
-        _ck(self.L.cairo_ctx_set_workgroups(self.h, rows, deblock), "set_workgroups")
+    def set_workgroups(self, rows: int = 0) -> None:
+        _ck(self.L.cairo_ctx_set_workgroups(self.h, rows), "set_workgroups")
 
 
 def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):

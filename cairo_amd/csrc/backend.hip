@@ -7,10 +7,10 @@
 //   table, inter  block table and per-(MB, ref) inter-search records
 //   sync          wavefront progress words, zeroed per frame
 // Per frame, on the kernels' stream:
-//   [H2D rgb] -> memset(sync) -> K0 convert -> K1 inter -> K2 rows -> K3 deblock
+//   [H2D rgb] -> memset(sync) -> K0 convert -> K1 inter -> K2 rows (+ deblock)
 // and on the copy stream, after K2: D2H of table + coefficients into a
 // pinned staging slot (the host entropy stage reads those while the GPU runs
-// the deblock and the next frames).
+// the next frames).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -29,12 +29,14 @@ constexpr int kStages = 8;
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,
               kInvalidResource = 8;
 
+constexpr int kTimed = 3;  // timed kernels: convert, inter search, mb rows (+deblock)
+
 struct Stage {
   uint8_t* table = nullptr;  // pinned
   int16_t* coef = nullptr;   // pinned, 1.5 * wa * ha
   int32_t* err = nullptr;    // pinned, 1 word
   hipEvent_t k2_done = nullptr, d2h_done = nullptr;
-  hipEvent_t ev[5] = {};  // kernel boundaries of this frame (profiling)
+  hipEvent_t ev[kTimed + 1] = {};  // kernel boundaries of this frame (profiling)
   bool timed = false;     // ev[] recorded, not yet collected
   int ticket = -1;
   bool busy = false;
@@ -55,9 +57,9 @@ struct cairo_ctx {
   size_t sync_words = 0;
   Stage st[kStages];
   int next_ticket = 0;
-  int wg_rows = 0, wg_deblock = 0;
+  int wg_rows = 0;
   bool profiling = false;
-  double acc_ms[4] = {0, 0, 0, 0};
+  double acc_ms[kTimed] = {0, 0, 0};
   int acc_frames = 0;
   bool have_inter = false;
   int16_t* predeblock = nullptr;  // debug snapshot of the slot after K2 (opt-in)
@@ -146,6 +148,10 @@ void free_ctx(cairo_ctx* c) {
   delete c;
 }
 
+size_t stamp_words(const cairo_ctx* c) {
+  return (size_t)c->wmb * c->hmb * kStampPhases + (size_t)c->hmb * kDbStamps + 2;
+}
+
 int zero_state(cairo_ctx* c) {
   CK(hipMemsetAsync(c->in, 0, c->plane_elems * 2, c->ks));
   CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2, c->ks));
@@ -164,8 +170,10 @@ int zero_state(cairo_ctx* c) {
 extern "C" {
 
 int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device, cairo_ctx** out) {
+  // The reference indexes blocks with uint16 (deblock.cpp, serialize.cpp): at
+  // most 65535 macroblocks per frame.
   if (!out || width == 0 || height == 0 || (width & 1) || (height & 1) || ring < 1 ||
-      ring > (uint32_t)kMaxRing)
+      ring > (uint32_t)kMaxRing || ((width + 15) / 16) * ((height + 15) / 16) > 65535u)
     return kInvalidArg;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
@@ -243,10 +251,9 @@ int cairo_ctx_reset(cairo_ctx* c) {
 
 int cairo_ctx_stages(const cairo_ctx*) { return kStages; }
 
-int cairo_ctx_set_workgroups(cairo_ctx* c, int rows, int deblock) {
+int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
   if (!c) return kInvalidArg;
   c->wg_rows = rows;
-  c->wg_deblock = deblock;
   return kSuccess;
 }
 
@@ -258,8 +265,8 @@ int cairo_ctx_set_profiling(cairo_ctx* c, int enable) {
 
 static int collect_times(cairo_ctx* c, Stage& s) {
   if (!s.timed) return kSuccess;
-  CK(hipEventSynchronize(s.ev[4]));
-  for (int k = 0; k < 4; k++) {
+  CK(hipEventSynchronize(s.ev[kTimed]));
+  for (int k = 0; k < kTimed; k++) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, s.ev[k], s.ev[k + 1]));
     c->acc_ms[k] += ms;
@@ -269,14 +276,14 @@ static int collect_times(cairo_ctx* c, Stage& s) {
   return kSuccess;
 }
 
-int cairo_ctx_take_timings(cairo_ctx* c, double ms[4], int* frames) {
+int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
   for (auto& s : c->st) {
     int r = collect_times(c, s);
     if (r) return r;
   }
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < kTimed; k++) {
     if (ms) ms[k] = c->acc_ms[k];
     c->acc_ms[k] = 0;
   }
@@ -318,17 +325,17 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   if (a.inter && c->ring > 1) CK(launch_inter_search(a, c->ks));
   c->have_inter = a.inter && c->ring > 1;
   if (prof) CK(hipEventRecord(s.ev[2], c->ks));
-  CK(launch_mb_rows(a, c->wg_rows, c->ks));
-  if (prof) CK(hipEventRecord(s.ev[3], c->ks));
-  CK(hipEventRecord(s.k2_done, c->ks));
-  if (c->predeblock)
-    CK(hipMemcpyAsync(c->predeblock, c->ring_buf + (size_t)(index % c->ring) * c->plane_elems,
-                      c->plane_elems * 2, hipMemcpyDeviceToDevice, c->ks));
-  CK(launch_deblock(a, c->wg_deblock, c->ks));
+  if (c->stamps) {  // kernel entry (min) / exit (max) words
+    const uint64_t init[2] = {~0ull, 0};
+    CK(hipMemcpyAsync(c->stamps + stamp_words(c) - 2, init, sizeof(init), hipMemcpyHostToDevice, c->ks));
+  }
+  CK(launch_mb_rows(a, c->wg_rows, c->ks));  // coding + in-loop deblock
   if (prof) {
-    CK(hipEventRecord(s.ev[4], c->ks));
+    CK(hipEventRecord(s.ev[3], c->ks));
     s.timed = true;
   }
+  CK(hipEventRecord(s.k2_done, c->ks));
+  if (c->predeblock) CK(launch_unpack_granules(a, planes_at(c->predeblock, c), c->ks));
   // Outputs for the host entropy stage.
   const size_t mbs = (size_t)c->wmb * c->hmb;
   CK(hipStreamWaitEvent(c->cs, s.k2_done, 0));
@@ -416,7 +423,7 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
   CK(hipSetDevice(c->device));
   if ((flags & 1) && !c->predeblock) CK(hipMalloc(&c->predeblock, c->plane_elems * 2));
   if ((flags & 2) && !c->stamps)
-    CK(hipMalloc(&c->stamps, (size_t)c->wmb * c->hmb * kStampPhases * sizeof(uint64_t)));
+    CK(hipMalloc(&c->stamps, stamp_words(c) * sizeof(uint64_t)));
   return kSuccess;
 }
 
@@ -424,8 +431,7 @@ int cairo_ctx_read_stamps(cairo_ctx* c, uint64_t* out) {
   if (!c || !c->stamps || !out) return kInvalidArg;
   CK(hipSetDevice(c->device));
   CK(hipStreamSynchronize(c->ks));
-  CK(hipMemcpy(out, c->stamps, (size_t)c->wmb * c->hmb * kStampPhases * sizeof(uint64_t),
-               hipMemcpyDeviceToHost));
+  CK(hipMemcpy(out, c->stamps, stamp_words(c) * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return kSuccess;
 }
 

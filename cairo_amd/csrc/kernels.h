@@ -47,6 +47,7 @@ struct FrameArgs {
   uint64_t* stamps;        // diagnostic: per-MB phase timestamps (nullptr = off)
   uint64_t* granules;      // K2 hand-off: 192 {tag, 2 px} granules per macroblock
   uint32_t epoch;          // granule tag of this frame (per-context submission count)
+  int row_workers;         // k_mb_rows: workgroups [0, row_workers) code rows, the rest deblock
 };
 
 // Granule hand-off of a reconstructed macroblock (MI355X_MICROARCH.md, R2 form):
@@ -58,22 +59,29 @@ constexpr int kGranulesPerMB = 192;
 
 // Phase boundaries recorded per macroblock by k_mb_rows when stamps != nullptr.
 constexpr int kStampPhases = 12;  // 10 real-time stamps + 2 shader-clock stamps
+// ...followed by kDbStamps per MB row: deblock worker phases 0..7, and 8 = the
+// row worker's "row coded" publish.
+constexpr int kDbStamps = 9;
 
 // Words of FrameArgs::sync (all int32, zeroed per frame).
 struct SyncLayout {
   static constexpr int kErr = 0;         // nonzero: a bounded wait timed out
   static constexpr int kRowTicket = 1;   // K2 row dequeue
-  static constexpr int kDbTicket = 2;    // K3 band dequeue, 3 planes
-  static constexpr int kRowDone = 8;     // K2 per-row progress [hmb]
-  // K3 per-band progress for plane p at kRowDone + hmb + p * max_bands
-  __host__ __device__ static int words(int hmb) { return kRowDone + hmb + 3 * (2 * hmb + 2) + 8; }
-  __host__ __device__ static int db_base(int hmb, int plane) { return kRowDone + hmb + plane * (2 * hmb + 2); }
+  static constexpr int kDbTicket = 2;    // deblock row dequeue
+  static constexpr int kRowCoded = 8;    // [hmb]: MB row r coded (release/acquire)
+  __host__ __device__ static int deblocked(int hmb) { return kRowCoded + hmb; }  // [hmb]
+  __host__ __device__ static int words(int hmb) { return kRowCoded + 2 * hmb + 8; }
 };
+
+// Deblock workers appended to the row workers of k_mb_rows.
+constexpr int kDeblockWorkers = 4;
 
 hipError_t launch_convert(const FrameArgs& a, hipStream_t s);
 hipError_t launch_inter_search(const FrameArgs& a, hipStream_t s);
 hipError_t launch_mb_rows(const FrameArgs& a, int workgroups, hipStream_t s);
-hipError_t launch_deblock(const FrameArgs& a, int workgroups, hipStream_t s);
+// Debug: rebuild the pre-deblock reconstruction of the last frame from the
+// K2 granules into plane set dst.
+hipError_t launch_unpack_granules(const FrameArgs& a, PlaneSet dst, hipStream_t s);
 
 // Known-answer entry points: apply the device transform / quantizer code to
 // a batch of macroblocks (6 blocks of 64 int16 each, block-major).

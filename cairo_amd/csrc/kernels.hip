@@ -626,6 +626,190 @@ __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool i
 }
 
 // ---------------------------------------------------------------------------
+// Deblocking (deblock.cpp:201-284), fused into the row workers of K2.  The
+// reference filters in place in raster order: per 8-row band, for each 8-px
+// unit x the horizontal edge H(x) (top of the band) then the vertical edge V(x)
+// (left of the unit).  H(x) touches only columns x..x+7 (rows y-3..y+2) and
+// V(x) columns x-3..x+2, so within a band every H is independent of every V
+// but its own and its left neighbour's: all H edges of a band, then all V
+// edges, is the raster result.  Band b+1's H edges read rows that band b's V
+// edges wrote, so bands run in order.  MB row r owns luma bands 2r, 2r+1 and
+// chroma band r; it is filtered by the workgroup that coded it, after row r-1
+// is fully filtered, while later rows keep coding: they read the current
+// frame only through granules (pre-deblock values), and their stale row below
+// has not been touched yet.
+// ---------------------------------------------------------------------------
+
+// deblock_filter_values on 8 samples v[0..7] = p3 p2 p1 p0 q0 q1 q2 q3, in registers.
+__device__ __forceinline__ void dfilter_reg(int* v, int qp, int strength, bool luma) {
+  const int p3 = v[0], p2 = v[1], p1 = v[2], p0 = v[3], q0 = v[4], q1 = v[5], q2 = v[6], q3 = v[7];
+  const int16_t dpq = (int16_t)iabs(p0 - q0), dp = (int16_t)iabs(p1 - p0), dq = (int16_t)iabs(q1 - q0);
+  if (strength == 0 || dpq >= kAlpha[qp] || dp >= kBeta[qp] || dq >= kBeta[qp]) return;
+  if (strength == 2) {
+    v[3] = (int16_t)rdiv(p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1, 8);
+    v[2] = (int16_t)rdiv(p2 + p1 + p0 + q0, 4);
+    v[4] = (int16_t)rdiv(p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2, 8);
+    v[5] = (int16_t)rdiv(p0 + q0 + q1 + q2, 4);
+    if (luma) {
+      v[1] = (int16_t)rdiv(2 * p3 + 3 * p2 + p1 + p0 + q0, 8);
+      v[6] = (int16_t)rdiv(2 * q3 + 3 * q2 + q1 + q0 + p0, 8);
+    }
+  } else {
+    v[3] = (int16_t)rdiv(((q0 + p0) * 4) + p1 - q1, 8);
+    v[4] = (int16_t)rdiv(((q0 + p0) * 4) + q1 - p1, 8);
+    if (luma) {
+      v[2] = (int16_t)rdiv((p2 * 4) + (p0 * 2) + (q0 * 2), 8);
+      v[5] = (int16_t)rdiv((q2 * 4) + (q0 * 2) + (p0 * 2), 8);
+    }
+  }
+}
+
+// Edge strength and qp (compute_deblock_strength / compute_average_qp,
+// deblock.cpp:49-79) from the LDS row cache: entry = copy << 8 | q_index.
+__device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
+  const bool cl = l >> 8, cr = r >> 8;
+  const int ql = l & 0xFF, qr = r & 0xFF;
+  qp = (!cl && !cr) ? ((ql + qr) >> 1) : (!cl ? ql : (!cr ? qr : 0));
+  return (cl && cr) ? 0 : ((cl != cr) ? 1 : 2);
+}
+
+// One deblock phase over a plane: n independent 8-sample lines.  Line i is
+// the 8 samples around an edge; `at(i)` gives its centre (the first q sample)
+// and `q(i, l, r)` the table-cache entries on both sides.  Vertical edges
+// (kRow: the line runs along a pixel row) load and store each line as two
+// 8-byte words; horizontal edges (column lines, stride `width`) one int16 per
+// lane per row, coalesced across lanes.  Every line of this thread's batch is
+// loaded before any is filtered, and lines of one phase never overlap (see
+// above), so whole lines are stored back.
+template <bool kRow, int kB, typename At, typename Q>
+__device__ __forceinline__ void db_phase(int16_t* img, int n, int width, bool luma, const int16_t* dq,
+                                         At at, Q q) {
+  for (int i0 = 0; i0 < n; i0 += 256 * kB) {
+    int v[kB][8], st[kB], qp[kB];
+    size_t off[kB];
+#pragma unroll
+    for (int b = 0; b < kB; b++) {
+      const int i = i0 + b * 256 + (int)threadIdx.x;
+      st[b] = 0;
+      if (i < n) {
+        off[b] = at(i);
+        int lq, rq;
+        q(i, lq, rq);
+        st[b] = edge_strength_q(dq[lq], dq[rq], qp[b]);
+        if (kRow) {
+          const short4 lo = *(const short4*)(img + off[b] - 4), hi = *(const short4*)(img + off[b]);
+          v[b][0] = lo.x, v[b][1] = lo.y, v[b][2] = lo.z, v[b][3] = lo.w;
+          v[b][4] = hi.x, v[b][5] = hi.y, v[b][6] = hi.z, v[b][7] = hi.w;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++) v[b][k] = img[off[b] + (ptrdiff_t)(k - 4) * width];
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < kB; b++) {
+      if (!st[b]) continue;
+      int w[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) w[k] = v[b][k];
+      dfilter_reg(w, qp[b], st[b], luma);
+      if (kRow) {
+        if (w[1] != v[b][1] || w[2] != v[b][2] || w[3] != v[b][3] || w[4] != v[b][4] ||
+            w[5] != v[b][5] || w[6] != v[b][6]) {
+          *(short4*)(img + off[b] - 4) = make_short4(w[0], w[1], w[2], w[3]);
+          *(short4*)(img + off[b]) = make_short4(w[4], w[5], w[6], w[7]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 1; k < 7; k++)
+          if (w[k] != v[b][k]) img[off[b] + (ptrdiff_t)(k - 4) * width] = (int16_t)w[k];
+      }
+    }
+  }
+}
+
+// Horizontal edges at row j (column filters) / vertical edges of the band at
+// row j (row filters, units x >= 1) of one plane.  dq: table cache of MB rows
+// (j / mbsz) - 1 (entries 0..wib-1) and j / mbsz (entries wib..2*wib-1).
+__device__ __forceinline__ void db_h(int16_t* img, int width, int mbsz, int j, bool luma,
+                                     const int16_t* dq, bool interior) {
+  const int wib = width / mbsz;
+  db_phase<false, 4>(img, width, width, luma, dq,
+                     [=](int col) { return (size_t)j * width + col; },
+                     [=](int col, int& l, int& r) {
+                       l = (interior ? wib : 0) + col / mbsz;
+                       r = wib + col / mbsz;
+                     });
+}
+__device__ __forceinline__ void db_v(int16_t* img, int width, int mbsz, int j, bool luma,
+                                     const int16_t* dq) {
+  const int wib = width / mbsz;
+  db_phase<true, 4>(img, width - 8, width, luma, dq,
+                    [=](int i) { return (size_t)(j + (i & 7)) * width + ((i >> 3) + 1) * 8; },
+                    [=](int i, int& l, int& r) {
+                      const int x = (i >> 3) + 1;
+                      l = wib + (x * 8 - 1) / mbsz;
+                      r = wib + (x * 8) / mbsz;
+                    });
+}
+
+// Deblock worker: MB rows in order, each once row r is coded and row r-1 is
+// filtered.  Row workers never wait on deblock workers (no deadlock).
+// dq: LDS scratch of 2 * wmb int16.
+__device__ __forceinline__ void deblock_rows(const FrameArgs& a, int16_t* dq, int* slot) {
+  const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
+  int32_t* err = a.sync + SyncLayout::kErr;
+  int32_t* coded = a.sync + SyncLayout::kRowCoded;
+  int32_t* done = a.sync + SyncLayout::deblocked(a.hmb);
+  const int cw = a.wa >> 1;
+  for (;;) {
+    const int r = dequeue(a.sync + SyncLayout::kDbTicket, slot);
+    if (r >= a.hmb) break;
+    uint64_t* ds = a.stamps ? a.stamps + (size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps : nullptr;
+#define DB_STAMP(k) \
+  if (ds && threadIdx.x == 0) ds[k] = __builtin_amdgcn_s_memrealtime();
+    DB_STAMP(0);
+    if (threadIdx.x == 0) {
+      wait_at_least(&coded[r], 1, err, a.sticky);
+      if (r > 0) wait_at_least(&done[r - 1], 1, err, a.sticky);
+    }
+    DB_STAMP(1);
+    acquire_after_wait();
+    DB_STAMP(2);
+    for (int i = threadIdx.x; i < 2 * a.wmb; i += 256) {
+      const int row = r - 1 + (i >= a.wmb), col = i >= a.wmb ? i - a.wmb : i;
+      int e = 0;
+      if (row >= 0) {
+        const BlockDesc& d = a.table[row * a.wmb + col];
+        e = ((d.block_type & kCopy) ? 0x100 : 0) | d.q_index;
+      }
+      dq[i] = (int16_t)e;
+    }
+    __syncthreads();
+    DB_STAMP(3);
+    if (r > 0) {  // band 2r (luma) / r (chroma): top edges, then vertical edges
+      db_h(cs.y, a.wa, 16, 16 * r, true, dq, false);
+      db_h(cs.u, cw, 8, 8 * r, false, dq, false);
+      db_h(cs.v, cw, 8, 8 * r, false, dq, false);
+    }
+    __syncthreads();
+    DB_STAMP(4);
+    db_v(cs.y, a.wa, 16, 16 * r, true, dq);
+    db_v(cs.u, cw, 8, 8 * r, false, dq);
+    db_v(cs.v, cw, 8, 8 * r, false, dq);
+    __syncthreads();
+    DB_STAMP(5);
+    db_h(cs.y, a.wa, 16, 16 * r + 8, true, dq, true);  // band 2r+1: MB-interior edge
+    __syncthreads();
+    DB_STAMP(6);
+    db_v(cs.y, a.wa, 16, 16 * r + 8, true, dq);
+    publish(&done[r], 1);
+    DB_STAMP(7);
+#undef DB_STAMP
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K2: the macroblock wavefront.  One workgroup owns one macroblock row at a
 // time (dequeued in order) and walks it left to right.  MB (bx, by) starts
 // when row by-1 has finished MB bx+2, i.e. the schedule t = bx + 3*by that
@@ -808,6 +992,16 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
   const int mbs = a.wmb * a.hmb;
+  uint64_t* ks = a.stamps ? a.stamps + (size_t)mbs * kStampPhases + (size_t)a.hmb * kDbStamps : nullptr;
+  if (ks && tid == 0) {  // kernel entry (min) / exit (max) over workgroups
+    __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if ((int)blockIdx.x >= a.row_workers) {  // in-loop deblock workers
+    deblock_rows(a, L.win.y, &L.slot);
+    if (ks && tid == 0)
+      __hip_atomic_fetch_max(&ks[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
 
   for (;;) {
     const int by = dequeue(a.sync + SyncLayout::kRowTicket, &L.slot);
@@ -1060,115 +1254,43 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
       stamp(a, mb, 9);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
+    publish(&a.sync[SyncLayout::kRowCoded + by], 1);  // row by coded: the deblock may start
+    if (a.stamps && tid == 0)
+      a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)by * kDbStamps + 8] = __builtin_amdgcn_s_memrealtime();
   }
+  if (ks && tid == 0)
+    __hip_atomic_fetch_max(&ks[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-hipError_t launch_mb_rows(const FrameArgs& a, int workgroups, hipStream_t s) {
+__global__ __launch_bounds__(192) void k_unpack_granules(FrameArgs a, PlaneSet dst) {
+  const int mb = blockIdx.x, k = threadIdx.x;
+  const int mbx = mb % a.wmb, mby = mb / a.wmb;
+  const uint32_t v = (uint32_t)a.granules[(size_t)mb * kGranulesPerMB + k];
+  int16_t* p;
+  if (k < 128) {
+    p = dst.y + (size_t)(mby * 16 + (k >> 3)) * a.wa + mbx * 16 + 2 * (k & 7);
+  } else {
+    const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
+    p = (pl ? dst.v : dst.u) + (size_t)(mby * 8 + r) * (a.wa >> 1) + mbx * 8 + 2 * d;
+  }
+  p[0] = (int16_t)(v & 0xFFFF);
+  p[1] = (int16_t)(v >> 16);
+}
+
+hipError_t launch_unpack_granules(const FrameArgs& a, PlaneSet dst, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack_granules, dim3(a.wmb * a.hmb), dim3(kGranulesPerMB), 0, s, a, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_mb_rows(const FrameArgs& a0, int workgroups, hipStream_t s) {
+  FrameArgs a = a0;
   int g = workgroups > 0 ? workgroups : a.hmb;
   if (g > a.hmb) g = a.hmb;
-  hipLaunchKernelGGL(k_mb_rows, dim3(g), dim3(256), 0, s, a);
+  a.row_workers = g;
+  hipLaunchKernelGGL(k_mb_rows, dim3(g + kDeblockWorkers), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// K3: deblocking (deblock.cpp:201-284).  One workgroup owns one 8-row band of
-// one plane at a time and walks it in chunks of 32 edge units; within a chunk
-// all horizontal edges run, then all vertical edges (equivalent to the raster
-// interleaving: V(x) only reads H(x-1), H(x)).  Band y's chunk [c, c+32)
-// starts when band y-1 has finished unit c+32 (t = x + 2y schedule).
-// ---------------------------------------------------------------------------
-
-constexpr int kDbChunk = 32;
-
-// deblock_filter_values (deblock.cpp:81-129) on one line through an edge.
-__device__ __forceinline__ void dfilter(int16_t* p, int step, int qp, int strength, bool luma) {
-  const int p3 = p[-4 * step], p2 = p[-3 * step], p1 = p[-2 * step], p0 = p[-step];
-  const int q0 = p[0], q1 = p[step], q2 = p[2 * step], q3 = p[3 * step];
-  const int16_t dpq = (int16_t)iabs(p0 - q0), dp = (int16_t)iabs(p1 - p0),
-                dq = (int16_t)iabs(q1 - q0);
-  if (dpq >= kAlpha[qp] || dp >= kBeta[qp] || dq >= kBeta[qp]) return;
-  if (strength == 2) {
-    p[-step] = (int16_t)rdiv(p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1, 8);
-    p[-2 * step] = (int16_t)rdiv(p2 + p1 + p0 + q0, 4);
-    p[0] = (int16_t)rdiv(p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2, 8);
-    p[step] = (int16_t)rdiv(p0 + q0 + q1 + q2, 4);
-    if (luma) {
-      p[-3 * step] = (int16_t)rdiv(2 * p3 + 3 * p2 + p1 + p0 + q0, 8);
-      p[2 * step] = (int16_t)rdiv(2 * q3 + 3 * q2 + q1 + q0 + p0, 8);
-    }
-  } else {
-    p[-step] = (int16_t)rdiv(((q0 + p0) * 4) + p1 - q1, 8);
-    p[0] = (int16_t)rdiv(((q0 + p0) * 4) + q1 - p1, 8);
-    if (luma) {
-      p[-2 * step] = (int16_t)rdiv((p2 * 4) + (p0 * 2) + (q0 * 2), 8);
-      p[step] = (int16_t)rdiv((q2 * 4) + (q0 * 2) + (p0 * 2), 8);
-    }
-  }
-}
-
-// compute_average_qp / compute_deblock_strength (deblock.cpp:49-79).
-__device__ __forceinline__ int edge_strength(const BlockDesc& l, const BlockDesc& r, int& qp) {
-  const bool cl = (l.block_type & kCopy) != 0, cr = (r.block_type & kCopy) != 0;
-  qp = (!cl && !cr) ? ((l.q_index + r.q_index) >> 1) : (!cl ? l.q_index : (!cr ? r.q_index : 0));
-  return (cl && cr) ? 0 : ((cl != cr) ? 1 : 2);
-}
-
-__global__ __launch_bounds__(256) void k_deblock(FrameArgs a) {
-  __shared__ int slot;
-  const int plane = blockIdx.y;
-  const bool luma = plane == 0;
-  const int mbsz = luma ? 16 : 8;
-  const int width = luma ? a.wa : (a.wa >> 1), height = luma ? a.ha : (a.ha >> 1);
-  const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
-  int16_t* img = plane == 0 ? cs.y : (plane == 1 ? cs.u : cs.v);
-  const int nx = width / 8, nbands = height / 8;
-  const int wib = width / mbsz;
-  int32_t* err = a.sync + SyncLayout::kErr;
-  int32_t* prog = a.sync + SyncLayout::db_base(a.hmb, plane);
-  for (;;) {
-    const int band = dequeue(a.sync + SyncLayout::kDbTicket + plane, &slot);
-    if (band >= nbands) break;
-    const int j = band * 8;
-    for (int c = 0; c < nx; c += kDbChunk) {
-      const int cend = min(c + kDbChunk, nx);
-      if (band > 0) {
-        if (threadIdx.x == 0) wait_at_least(&prog[band - 1], min(cend + 1, nx), err, a.sticky);
-        acquire_after_wait();
-        // horizontal edges H(x, j), x in [c, cend): column filters
-        const int x = c + (threadIdx.x >> 3);
-        if (x < cend) {
-          const int col = x * 8 + (threadIdx.x & 7);
-          const uint32_t li = (uint32_t)((x * 8) / mbsz + ((j - 1) / mbsz) * wib);
-          const uint32_t ri = (uint32_t)((x * 8) / mbsz + (j / mbsz) * wib);
-          int qp;
-          const int st = edge_strength(a.table[(uint16_t)li], a.table[(uint16_t)ri], qp);
-          if (st) dfilter(img + (size_t)j * width + col, width, qp, st, luma);
-        }
-        __syncthreads();
-      }
-      // vertical edges V(x, j), x in [max(c,1), cend): row filters
-      {
-        const int x = c + (threadIdx.x >> 3);
-        if (x >= 1 && x < cend) {
-          const int row = j + (threadIdx.x & 7);
-          const uint32_t li = (uint32_t)((x * 8 - 1) / mbsz + (j / mbsz) * wib);
-          const uint32_t ri = (uint32_t)((x * 8) / mbsz + (j / mbsz) * wib);
-          int qp;
-          const int st = edge_strength(a.table[(uint16_t)li], a.table[(uint16_t)ri], qp);
-          if (st) dfilter(img + (size_t)row * width + x * 8, 1, qp, st, luma);
-        }
-      }
-      publish(&prog[band], cend);
-    }
-  }
-}
-
-hipError_t launch_deblock(const FrameArgs& a, int workgroups, hipStream_t s) {
-  int g = workgroups > 0 ? workgroups : (a.ha / 8);
-  if (g > a.ha / 8) g = a.ha / 8;
-  hipLaunchKernelGGL(k_deblock, dim3(g, 3), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------
 // KAT: transform/quantize/reconstruct chain on independent macroblocks.

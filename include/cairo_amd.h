@@ -8,7 +8,7 @@
  *     inside engine_encode_frame (reference encode.cpp:205-232): convert_image
  *     (convert.cpp:95-160), encode_slice (encode.cpp:165-203, with
  *     motion.cpp / transform.cpp / quantize.cpp / decode.cpp:15-144) and
- *     deblock_image_filter (deblock.cpp:277-284).  Its outputs are exactly what
+ *     deblock_image_filter (deblock.cpp:277-284, fused into the row kernel).  Its outputs are exactly what
  *     the host entropy stage serialize_slice (serialize.cpp:319-340) consumes:
  *     the block table (evx_block_desc[], common.h:78-95, 16 B each) and the
  *     persistent quantized-coefficient planes (output_cache, common.h:108).
@@ -83,11 +83,12 @@ CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, 
 
 /* Per-kernel timing (HIP events on the kernels' stream), opt-in. */
 CAIRO_API int cairo_ctx_set_profiling(cairo_ctx *ctx, int enable);
-/* Accumulated ms per kernel since the last call: [convert, inter, mb_rows,
- * deblock], and the number of frames they cover; resets the accumulators. */
-CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[4], int *frames);
-/* Workgroup counts of the wavefront kernels (0 = default). */
-CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows, int deblock);
+/* Accumulated ms per kernel since the last call: [convert, inter search,
+ * macroblock rows (coding + in-loop deblock)], and the number of frames they
+ * cover; resets the accumulators. */
+CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[3], int *frames);
+/* Workgroup count of the macroblock-row kernel (0 = one per MB row). */
+CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows);
 
 /* Known-answer check of the device transform chain: count macroblocks of 384
  * int16 (block-major: Y TL,TR,BL,BR, U, V; 64 each).  qtype[2m] = block type,

@@ -27,7 +27,9 @@ ctx.set_debug(2)
 for t in range(a.frames):
     ctx.encode_frame(cairo_amd.make_band4(w, h, t), t, t > 0, q)
     ctx.sync()
-st = ctx.read_stamps().astype(np.int64)  # (hmb, wmb, 10), 10 ns ticks
+st, dbs, kio = ctx.read_stamps()  # 10 ns ticks
+kio = kio.astype(np.int64)
+st, dbs = st.astype(np.int64), dbs.astype(np.int64)
 d = np.diff(st[..., :10], axis=2) / 100.0  # us
 print(f"{a.config} frame {a.frames - 1}: per-MB phase means (us) over {st.shape[0] * st.shape[1]} MBs")
 for k, name in enumerate(PHASES):
@@ -47,3 +49,13 @@ clk = (st[..., 11] - st[..., 10]) / np.maximum(st[..., 9] - st[..., 0], 1) * 100
 print(f"  effective shader clock: mean {clk.mean():.0f} MHz, p10 {np.percentile(clk, 10):.0f}, p90 {np.percentile(clk, 90):.0f}")
 span = (st[..., 9].max() - st[..., 0].min()) / 100.0
 print(f"  kernel span {span:.1f} us, steps {wb + 3 * (hb - 1)}, per step {span / (wb + 3 * (hb - 1)):.3f} us")
+# deblock workers: per row, phases relative to the row-coded publish (stamp 8)
+DBP = ["wait", "acquire", "table", "H band0", "V band0", "H band1", "V band1+pub"]
+dd = np.diff(dbs[:, :8], axis=1) / 100.0
+print("deblock per row (us): " + ", ".join(f"{n} {dd[:, k].mean():.2f}" for k, n in enumerate(DBP)))
+lag = (dbs[:, 7] - dbs[:, 8]) / 100.0
+print(f"  row coded -> row deblocked: mean {lag.mean():.2f} us, last row {lag[-1]:.2f} us")
+print(f"  last MB end -> last row deblocked: {(dbs[:, 7].max() - st[..., 9].max()) / 100.0:.2f} us")
+print(f"  kernel entry -> first MB: {(st[..., 0].min() - kio[0]) / 100.0:.2f} us; "
+      f"last row deblocked -> kernel exit: {(kio[1] - dbs[:, 7].max()) / 100.0:.2f} us; "
+      f"entry -> exit {(kio[1] - kio[0]) / 100.0:.1f} us")

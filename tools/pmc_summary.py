@@ -23,7 +23,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHORT = {"k_convert": "convert", "k_inter_search": "inter_search", "k_mb_rows": "mb_rows", "k_deblock": "deblock"}
+SHORT = {"k_convert": "convert", "k_inter_search": "inter_search", "k_mb_rows": "mb_rows"}
 
 
 def per_kernel(path):
