@@ -77,6 +77,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_set_profiling": (I, [P, I]),
         "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
         "cairo_ctx_set_workgroups": (I, [P, I]),
+        "cairo_ctx_set_batch": (I, [P, I]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "evx_encoder_create": (I, [ctypes.POINTER(P)]),
@@ -163,6 +164,7 @@ class Context:
         p = ctypes.c_void_p()
         _ck(self.L.cairo_ctx_create(width, height, ring, device, ctypes.byref(p)), "cairo_ctx_create")
         self.h = p
+        self._keep = {}  # ticket -> host RGB frame still being copied
 
     def close(self) -> None:
         if self.h:
@@ -182,11 +184,14 @@ class Context:
             self.L.cairo_ctx_submit(self.h, ptr, int(on_device), index, int(inter), quality, ctypes.byref(t)),
             "cairo_ctx_submit",
         )
+        if not on_device:  # the H2D copy is asynchronous: keep the host frame alive
+            self._keep[t.value] = rgb
         return t.value
 
     def wait(self, ticket: int, copy: bool = True) -> FrameOutputs:
         r = _FrameResult()
         _ck(self.L.cairo_ctx_wait(self.h, ticket, ctypes.byref(r)), "cairo_ctx_wait")
+        self._keep.pop(ticket, None)
         ny, nc = r.wa * r.ha, (r.wa // 2) * (r.ha // 2)
         mbs = r.wmb * r.hmb
         out = FrameOutputs(
@@ -260,6 +265,9 @@ class Context:
         n = ctypes.c_int()
         _ck(self.L.cairo_ctx_take_timings(self.h, ms, ctypes.byref(n)), "take_timings")
         return list(ms), n.value
+
+    def set_batch(self, frames: int) -> None:
+        _ck(self.L.cairo_ctx_set_batch(self.h, frames), "set_batch")
 
     def set_workgroups(self, rows: int = 0) -> None:
         _ck(self.L.cairo_ctx_set_workgroups(self.h, rows), "set_workgroups")

@@ -1,22 +1,25 @@
 // cairo_amd/csrc/backend.hip -- device context and frame orchestration.
 //
-// One context = one encoder's device state in HBM (see DESIGN.md "Data layout"):
-//   input_cache   planes (convert output, read by both searches)
-//   output_cache  planes (quantized coefficients, persistent across frames)
-//   ring          R contiguous plane sets (reconstruction slots)
-//   table, inter  block table and per-(MB, ref) inter-search records
-//   sync          wavefront progress words, zeroed per frame
-// Per frame, on the kernels' stream:
-//   [H2D rgb] -> memset(sync) -> K0 convert -> K1 inter -> K2 rows (+ deblock)
-// and on the copy stream, after K2: D2H of table + coefficients into a
-// pinned staging slot (the host entropy stage reads those while the GPU runs
-// the next frames).
+// One context = one encoder's device state in HBM (DESIGN.md "Data layout"):
+//   ring          R contiguous plane sets (reconstruction slots, frame n -> n % R)
+//   16 staging slots, one per frame in flight, each with its own
+//     source planes (convert output), output_cache planes (coefficients),
+//     block table, inter-search records, granules, RGB staging and pinned
+//     host buffers for the table + coefficients
+//   sync          batch flags (zeroed per launch)
+// Frames are submitted into a batch (up to batch_max, default 8) that is
+// launched when full or when a caller waits on one of its frames:
+//   memset(sync) -> convert (all frames) -> engine (inter search, row coding,
+//   deblock, pipelined across the frames)
+// and on the copy stream, after the engine: D2H of each frame's table and
+// coefficients into its pinned staging (the host entropy stage reads those
+// while the GPU runs the next batch).
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "../../include/cairo_amd.h"
 #include "kernels.h"
@@ -25,22 +28,27 @@ using namespace cairo;
 
 namespace {
 
-constexpr int kStages = 8;
-constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,
+constexpr int kStages = 16;      // staging slots (frames in flight)
+constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
+constexpr int kDefaultBatch = 8;
+constexpr int kSuccess = 0, kInvalidArg = 2, kOutOfMemory = 3, kHardwareFail = 5,
               kInvalidResource = 8;
-
-constexpr int kTimed = 3;  // timed kernels: convert, inter search, mb rows (+deblock)
 
 struct Stage {
   uint8_t* table = nullptr;  // pinned
   int16_t* coef = nullptr;   // pinned, 1.5 * wa * ha
   int32_t* err = nullptr;    // pinned, 1 word
-  hipEvent_t k2_done = nullptr, d2h_done = nullptr;
-  hipEvent_t ev[kTimed + 1] = {};  // kernel boundaries of this frame (profiling)
-  bool timed = false;     // ev[] recorded, not yet collected
+  hipEvent_t d2h_done = nullptr;
   int ticket = -1;
-  bool busy = false;
+  bool busy = false;      // submitted, not yet released
+  bool launched = false;  // its batch has been launched
   uint32_t index = 0, type = 0, quality = 0;
+};
+
+struct TimedBatch {
+  hipEvent_t ev[kTimed + 1] = {};
+  int frames = 0;
+  bool pending = false;
 };
 
 }  // namespace
@@ -48,24 +56,33 @@ struct Stage {
 struct cairo_ctx {
   int device = 0;
   uint32_t w = 0, h = 0, wa = 0, ha = 0, wmb = 0, hmb = 0, ring = 0;
-  size_t plane_elems = 0;  // Y + U + V of one plane set
+  size_t plane_elems = 0, mbs = 0, nref = 1;
   hipStream_t ks = nullptr, cs = nullptr;
-  int16_t *in = nullptr, *coef = nullptr, *ring_buf = nullptr;
-  BlockDesc *table = nullptr, *inter_desc = nullptr;
-  int32_t *inter_sad = nullptr, *sync = nullptr, *sticky = nullptr;
+  hipEvent_t engine_done = nullptr;  // last launched batch finished (copy stream waits on it)
+  // per-slot device buffers
+  int16_t *src = nullptr, *coef = nullptr;
+  BlockDesc *table = nullptr, *idesc = nullptr;
+  int32_t* isad = nullptr;
+  uint64_t* gran = nullptr;
   uint8_t* rgb = nullptr;
+  int16_t* ring_buf = nullptr;
+  int32_t *sync = nullptr, *sticky = nullptr;
   size_t sync_words = 0;
   Stage st[kStages];
   int next_ticket = 0;
+  uint32_t epoch = 0;
+  int batch_max = kDefaultBatch;
+  FrameDesc pend[kMaxBatch];
+  int npend = 0;
+  int last_slot = -1;  // slot of the last launched frame
   int wg_rows = 0;
   bool profiling = false;
+  TimedBatch tb[kStages];
+  int tb_next = 0;
   double acc_ms[kTimed] = {0, 0, 0};
   int acc_frames = 0;
-  bool have_inter = false;
-  int16_t* predeblock = nullptr;  // debug snapshot of the slot after K2 (opt-in)
-  uint64_t* stamps = nullptr;     // diagnostic K2 phase stamps (opt-in)
-  uint64_t* granules = nullptr;   // K2 macroblock hand-off granules
-  uint32_t epoch = 0;             // granule tag of the last submitted frame
+  int16_t* predeblock = nullptr;  // debug: pre-deblock reconstruction of the last frame (opt-in)
+  uint64_t* stamps = nullptr;     // diagnostic phase stamps (opt-in)
 };
 
 namespace {
@@ -82,39 +99,33 @@ int fail(hipError_t e, const char* what) {
   } while (0)
 
 PlaneSet planes_at(int16_t* base, const cairo_ctx* c) {
-  PlaneSet p;
-  p.y = base;
-  p.u = base + (size_t)c->wa * c->ha;
-  p.v = p.u + (size_t)(c->wa / 2) * (c->ha / 2);
-  return p;
+  return ring_slot(base, 0, (int)c->wa, (int)c->ha, 0);
+}
+PlaneSet slot_planes(int16_t* base, const cairo_ctx* c, int slot) {
+  return ring_slot(base, c->plane_elems, (int)c->wa, (int)c->ha, slot);
 }
 
-FrameArgs frame_args(const cairo_ctx* c, uint32_t index, uint32_t type, uint32_t quality) {
-  FrameArgs a;
-  memset(&a, 0, sizeof(a));
-  a.wa = (int)c->wa;
-  a.ha = (int)c->ha;
-  a.w = (int)c->w;
-  a.h = (int)c->h;
-  a.wmb = (int)c->wmb;
-  a.hmb = (int)c->hmb;
-  a.ring = (int)c->ring;
-  a.index = (int)index;
-  a.inter = type == 1 ? 1 : 0;
-  a.quality = (int)quality;
-  a.rgb = c->rgb;
-  a.in = planes_at(c->in, c);
-  a.coef = planes_at(c->coef, c);
-  a.ring_base = c->ring_buf;
-  a.slot_elems = c->plane_elems;
-  a.table = c->table;
-  a.inter_desc = c->inter_desc;
-  a.inter_sad = c->inter_sad;
-  a.sync = c->sync;
-  a.sticky = c->sticky;
-  a.stamps = c->stamps;
-  a.granules = c->granules;
-  return a;
+size_t stamp_words(const cairo_ctx* c) {
+  return c->mbs * kStampPhases + (size_t)c->hmb * kDbStamps + 2;
+}
+
+EngineArgs engine_args(const cairo_ctx* c) {
+  EngineArgs e;
+  memset(&e, 0, sizeof(e));
+  e.wa = (int)c->wa, e.ha = (int)c->ha, e.w = (int)c->w, e.h = (int)c->h;
+  e.wmb = (int)c->wmb, e.hmb = (int)c->hmb, e.ring = (int)c->ring;
+  e.src_base = c->src;
+  e.coef_base = c->coef;
+  e.plane_elems = c->plane_elems;
+  e.table_base = c->table;
+  e.idesc_base = c->idesc;
+  e.isad_base = c->isad;
+  e.gran_base = c->gran;
+  e.ring_base = c->ring_buf;
+  e.sync = c->sync;
+  e.sticky = c->sticky;
+  e.stamps = c->stamps;
+  return e;
 }
 
 void free_ctx(cairo_ctx* c) {
@@ -126,42 +137,114 @@ void free_ctx(cairo_ctx* c) {
     if (s.table) (void)hipHostFree(s.table);
     if (s.coef) (void)hipHostFree(s.coef);
     if (s.err) (void)hipHostFree(s.err);
-    if (s.k2_done) (void)hipEventDestroy(s.k2_done);
     if (s.d2h_done) (void)hipEventDestroy(s.d2h_done);
-    for (auto& e : s.ev)
-      if (e) (void)hipEventDestroy(e);
   }
-  (void)hipFree(c->in);
-  (void)hipFree(c->coef);
-  (void)hipFree(c->ring_buf);
-  (void)hipFree(c->table);
-  (void)hipFree(c->inter_desc);
-  (void)hipFree(c->inter_sad);
-  (void)hipFree(c->sync);
-  (void)hipFree(c->sticky);
-  (void)hipFree(c->rgb);
-  (void)hipFree(c->predeblock);
-  (void)hipFree(c->stamps);
-  (void)hipFree(c->granules);
+  for (auto& t : c->tb)
+    for (auto& e : t.ev)
+      if (e) (void)hipEventDestroy(e);
+  if (c->engine_done) (void)hipEventDestroy(c->engine_done);
+  for (void* p : {(void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad,
+                  (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
+                  (void*)c->predeblock, (void*)c->stamps})
+    (void)hipFree(p);
   if (c->ks) (void)hipStreamDestroy(c->ks);
   if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
 }
 
-size_t stamp_words(const cairo_ctx* c) {
-  return (size_t)c->wmb * c->hmb * kStampPhases + (size_t)c->hmb * kDbStamps + 2;
-}
-
 int zero_state(cairo_ctx* c) {
-  CK(hipMemsetAsync(c->in, 0, c->plane_elems * 2, c->ks));
-  CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2, c->ks));
+  CK(hipMemsetAsync(c->src, 0, c->plane_elems * 2 * kStages, c->ks));
+  CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2 * kStages, c->ks));
   CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
-  CK(hipMemsetAsync(c->table, 0, (size_t)c->wmb * c->hmb * sizeof(BlockDesc), c->ks));
-  // granule tags start at 0; the n-th submission after a reset publishes tag n.
-  CK(hipMemsetAsync(c->granules, 0, (size_t)c->wmb * c->hmb * kGranulesPerMB * sizeof(uint64_t),
-                    c->ks));
+  CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * kStages, c->ks));
+  // granule tags start at 0; the n-th submission after a reset publishes tag n
+  CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranulesPerMB * sizeof(uint64_t) * kStages, c->ks));
   CK(hipStreamSynchronize(c->ks));
   c->epoch = 0;
+  c->last_slot = -1;
+  return kSuccess;
+}
+
+int collect_times(cairo_ctx* c, TimedBatch& t) {
+  if (!t.pending) return kSuccess;
+  CK(hipEventSynchronize(t.ev[kTimed]));
+  for (int k = 0; k < kTimed; k++) {
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, t.ev[k], t.ev[k + 1]));
+    c->acc_ms[k] += ms;
+  }
+  c->acc_frames += t.frames;
+  t.pending = false;
+  return kSuccess;
+}
+
+// Launch the pending batch.
+int flush(cairo_ctx* c) {
+  if (c->npend == 0) return kSuccess;
+  CK(hipSetDevice(c->device));
+  EngineArgs e = engine_args(c);
+  e.nframes = c->npend;
+  bool any_inter = false;
+  for (int i = 0; i < c->npend; i++) {
+    e.fr[i] = c->pend[i];
+    any_inter |= e.fr[i].inter && c->ring > 1;
+  }
+  const int rows = e.nframes * e.hmb;
+  const int ng = (e.wmb + 3) / 4;
+  e.n_rows = c->wg_rows > 0 ? c->wg_rows : rows;
+  if (e.n_rows > 240) e.n_rows = 240;
+  if (e.n_rows > rows) e.n_rows = rows;
+  e.n_inter = any_inter ? rows * ng * (int)c->nref : 0;
+  if (e.n_inter > 64) e.n_inter = 64;
+  e.n_deblock = rows < 8 ? rows : 8;
+  TimedBatch* tb = nullptr;
+  if (c->profiling) {
+    tb = &c->tb[c->tb_next];
+    c->tb_next = (c->tb_next + 1) % kStages;
+    int r = collect_times(c, *tb);  // its events are about to be reused
+    if (r) return r;
+  }
+  CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t), c->ks));
+  if (c->stamps) {  // engine entry (min) / exit (max) words
+    static const uint64_t init[2] = {~0ull, 0};
+    CK(hipMemcpyAsync(c->stamps + stamp_words(c) - 2, init, sizeof(init), hipMemcpyHostToDevice, c->ks));
+  }
+  if (tb) CK(hipEventRecord(tb->ev[0], c->ks));
+  CK(launch_convert_batch(e, c->ks));
+  if (tb) CK(hipEventRecord(tb->ev[1], c->ks));
+  if (tb) CK(hipEventRecord(tb->ev[2], c->ks));
+  CK(launch_engine(e, c->ks));
+  if (tb) {
+    CK(hipEventRecord(tb->ev[3], c->ks));
+    tb->frames = e.nframes;
+    tb->pending = true;
+  }
+  const int last = e.fr[e.nframes - 1].slot;
+  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), c->ks));
+  // outputs for the host entropy stage, on the copy stream
+  CK(hipEventRecord(c->engine_done, c->ks));
+  CK(hipStreamWaitEvent(c->cs, c->engine_done, 0));
+  for (int i = 0; i < e.nframes; i++) {
+    const int slot = e.fr[i].slot;
+    Stage& s = c->st[slot];
+    CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
+                      hipMemcpyDeviceToHost, c->cs));
+    CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2,
+                      hipMemcpyDeviceToHost, c->cs));
+    CK(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
+    CK(hipEventRecord(s.d2h_done, c->cs));
+    s.launched = true;
+  }
+  c->last_slot = last;
+  c->npend = 0;
+  return kSuccess;
+}
+
+int sync_all(cairo_ctx* c) {
+  int r = flush(c);
+  if (r) return r;
+  CK(hipStreamSynchronize(c->ks));
+  CK(hipStreamSynchronize(c->cs));
   return kSuccess;
 }
 
@@ -191,8 +274,8 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   c->hmb = c->ha / 16;
   c->ring = ring;
   c->plane_elems = (size_t)c->wa * c->ha * 3 / 2;
-  const size_t mbs = (size_t)c->wmb * c->hmb;
-  const size_t nref = ring > 1 ? ring - 1 : 1;
+  c->mbs = (size_t)c->wmb * c->hmb;
+  c->nref = ring > 1 ? ring - 1 : 1;
   c->sync_words = (size_t)SyncLayout::words((int)c->hmb);
   int r = kSuccess;
 #define TRY(x)                         \
@@ -206,25 +289,26 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   TRY(hipSetDevice(device));
   TRY(hipStreamCreateWithFlags(&c->ks, hipStreamNonBlocking));
   TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
-  TRY(hipMalloc(&c->in, c->plane_elems * 2));
-  TRY(hipMalloc(&c->coef, c->plane_elems * 2));
+  TRY(hipMalloc(&c->src, c->plane_elems * 2 * kStages));
+  TRY(hipMalloc(&c->coef, c->plane_elems * 2 * kStages));
   TRY(hipMalloc(&c->ring_buf, c->plane_elems * 2 * ring));
-  TRY(hipMalloc(&c->table, mbs * sizeof(BlockDesc)));
-  TRY(hipMalloc(&c->inter_desc, nref * mbs * sizeof(BlockDesc)));
-  TRY(hipMalloc(&c->inter_sad, nref * mbs * sizeof(int32_t)));
+  TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * kStages));
+  TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * kStages));
+  TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * kStages));
+  TRY(hipMalloc(&c->gran, c->mbs * kGranulesPerMB * sizeof(uint64_t) * kStages));
+  TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * kStages));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t)));
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
-  TRY(hipMalloc(&c->granules, mbs * kGranulesPerMB * sizeof(uint64_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
-  TRY(hipMalloc(&c->rgb, (size_t)width * height * 3));
   for (auto& s : c->st) {
-    TRY(hipHostMalloc(&s.table, mbs * sizeof(BlockDesc), hipHostMallocDefault));
+    TRY(hipHostMalloc(&s.table, c->mbs * sizeof(BlockDesc), hipHostMallocDefault));
     TRY(hipHostMalloc(&s.coef, c->plane_elems * 2, hipHostMallocDefault));
     TRY(hipHostMalloc(&s.err, sizeof(int32_t), hipHostMallocDefault));
-    TRY(hipEventCreateWithFlags(&s.k2_done, hipEventDisableTiming));
     TRY(hipEventCreateWithFlags(&s.d2h_done, hipEventDisableTiming));
-    for (auto& e : s.ev) TRY(hipEventCreate(&e));
   }
+  for (auto& t : c->tb)
+    for (auto& e : t.ev) TRY(hipEventCreate(&e));
+  TRY(hipEventCreateWithFlags(&c->engine_done, hipEventDisableTiming));
 #undef TRY
   r = zero_state(c);
   if (r != kSuccess) {
@@ -244,15 +328,24 @@ int cairo_ctx_destroy(cairo_ctx* c) {
 int cairo_ctx_reset(cairo_ctx* c) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->cs));
+  int r = sync_all(c);
+  if (r) return r;
   for (auto& s : c->st) s.busy = false;
   return zero_state(c);
 }
 
 int cairo_ctx_stages(const cairo_ctx*) { return kStages; }
 
+int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
+  if (!c || frames < 1 || frames > kMaxBatch || frames > kStages / 2) return kInvalidArg;
+  int r = flush(c);
+  if (r) return r;
+  c->batch_max = frames;
+  return kSuccess;
+}
+
 int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
-  if (!c) return kInvalidArg;
+  if (!c || rows < 0) return kInvalidArg;
   c->wg_rows = rows;
   return kSuccess;
 }
@@ -263,24 +356,13 @@ int cairo_ctx_set_profiling(cairo_ctx* c, int enable) {
   return kSuccess;
 }
 
-static int collect_times(cairo_ctx* c, Stage& s) {
-  if (!s.timed) return kSuccess;
-  CK(hipEventSynchronize(s.ev[kTimed]));
-  for (int k = 0; k < kTimed; k++) {
-    float ms = 0;
-    CK(hipEventElapsedTime(&ms, s.ev[k], s.ev[k + 1]));
-    c->acc_ms[k] += ms;
-  }
-  c->acc_frames++;
-  s.timed = false;
-  return kSuccess;
-}
-
 int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  for (auto& s : c->st) {
-    int r = collect_times(c, s);
+  int r = flush(c);
+  if (r) return r;
+  for (auto& t : c->tb) {
+    r = collect_times(c, t);
     if (r) return r;
   }
   for (int k = 0; k < kTimed; k++) {
@@ -294,70 +376,51 @@ int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
 
 int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32_t index,
                      uint32_t type, uint32_t quality, int* ticket) {
-  if (!c || !rgb || quality < 1 || quality > 31 || type > 1) return kInvalidArg;
+  if (!c || !rgb || !ticket || quality < 1 || quality > 31 || type > 1) return kInvalidArg;
   CK(hipSetDevice(c->device));
   const int t = c->next_ticket;
-  Stage& s = c->st[t % kStages];
+  const int slot = t % kStages;
+  Stage& s = c->st[slot];
   if (s.busy) {
     fprintf(stderr, "[cairo_amd] staging slot of ticket %d not released\n", s.ticket);
     return kInvalidResource;
   }
-  {
-    int r = collect_times(c, s);  // this stage's events are about to be reused
-    if (r) return r;
-  }
-  FrameArgs a = frame_args(c, index, type, quality);
-  a.epoch = ++c->epoch;
+  FrameDesc& f = c->pend[c->npend];
   if (rgb_on_device) {
-    a.rgb = rgb;
+    f.rgb = rgb;
   } else {
-    CK(hipMemcpyAsync(c->rgb, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, c->ks));
+    uint8_t* dst = c->rgb + (size_t)slot * c->w * c->h * 3;
+    CK(hipMemcpyAsync(dst, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, c->ks));
+    f.rgb = dst;
   }
-  // K2 rewrites the coefficient planes and the block table, and the memset
-  // below clears the error word: the previous frame's D2H must have finished.
-  const Stage& prev = c->st[(t + kStages - 1) % kStages];
-  if (prev.ticket >= 0) CK(hipStreamWaitEvent(c->ks, prev.d2h_done, 0));
-  CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t), c->ks));
-  const bool prof = c->profiling;
-  if (prof) CK(hipEventRecord(s.ev[0], c->ks));
-  CK(launch_convert(a, c->ks));
-  if (prof) CK(hipEventRecord(s.ev[1], c->ks));
-  if (a.inter && c->ring > 1) CK(launch_inter_search(a, c->ks));
-  c->have_inter = a.inter && c->ring > 1;
-  if (prof) CK(hipEventRecord(s.ev[2], c->ks));
-  if (c->stamps) {  // kernel entry (min) / exit (max) words
-    const uint64_t init[2] = {~0ull, 0};
-    CK(hipMemcpyAsync(c->stamps + stamp_words(c) - 2, init, sizeof(init), hipMemcpyHostToDevice, c->ks));
-  }
-  CK(launch_mb_rows(a, c->wg_rows, c->ks));  // coding + in-loop deblock
-  if (prof) {
-    CK(hipEventRecord(s.ev[3], c->ks));
-    s.timed = true;
-  }
-  CK(hipEventRecord(s.k2_done, c->ks));
-  if (c->predeblock) CK(launch_unpack_granules(a, planes_at(c->predeblock, c), c->ks));
-  // Outputs for the host entropy stage.
-  const size_t mbs = (size_t)c->wmb * c->hmb;
-  CK(hipStreamWaitEvent(c->cs, s.k2_done, 0));
-  CK(hipMemcpyAsync(s.table, c->table, mbs * sizeof(BlockDesc), hipMemcpyDeviceToHost, c->cs));
-  CK(hipMemcpyAsync(s.coef, c->coef, c->plane_elems * 2, hipMemcpyDeviceToHost, c->cs));
-  CK(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
-  CK(hipEventRecord(s.d2h_done, c->cs));
+  f.index = (int)index;
+  f.inter = type == 1 ? 1 : 0;
+  f.quality = (int)quality;
+  f.epoch = ++c->epoch;
+  f.slot = slot;
+  f.prev_slot = (t + kStages - 1) % kStages;
+  c->npend++;
   s.busy = true;
+  s.launched = false;
   s.ticket = t;
   s.index = index;
   s.type = type;
   s.quality = quality;
   c->next_ticket++;
   *ticket = t;
+  if (c->npend >= c->batch_max) return flush(c);
   return kSuccess;
 }
 
 int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
-  if (!c || !out) return kInvalidArg;
+  if (!c || !out || ticket < 0) return kInvalidArg;
   Stage& s = c->st[ticket % kStages];
   if (!s.busy || s.ticket != ticket) return kInvalidResource;
   CK(hipSetDevice(c->device));
+  if (!s.launched) {
+    int r = flush(c);
+    if (r) return r;
+  }
   CK(hipEventSynchronize(s.d2h_done));
   if (*s.err) {
     fprintf(stderr, "[cairo_amd] an in-kernel wait timed out (at or before frame %u)\n", s.index);
@@ -378,7 +441,7 @@ int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
 }
 
 int cairo_ctx_release(cairo_ctx* c, int ticket) {
-  if (!c) return kInvalidArg;
+  if (!c || ticket < 0) return kInvalidArg;
   Stage& s = c->st[ticket % kStages];
   if (s.ticket != ticket) return kInvalidResource;
   s.busy = false;
@@ -388,18 +451,18 @@ int cairo_ctx_release(cairo_ctx* c, int ticket) {
 int cairo_ctx_sync(cairo_ctx* c) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->ks));
-  CK(hipStreamSynchronize(c->cs));
-  return kSuccess;
+  return sync_all(c);
 }
 
 int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16_t* v) {
   if (!c || which < 0 || which >= 2 + (int)c->ring) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->ks));
-  CK(hipStreamSynchronize(c->cs));
-  int16_t* base = which == 0 ? c->in : which == 1 ? c->coef : c->ring_buf + (size_t)(which - 2) * c->plane_elems;
-  PlaneSet p = planes_at(base, c);
+  int r = sync_all(c);
+  if (r) return r;
+  if (which < 2 && c->last_slot < 0) return kInvalidResource;
+  PlaneSet p = which == 0 ? slot_planes(c->src, c, c->last_slot)
+               : which == 1 ? slot_planes(c->coef, c, c->last_slot)
+                            : slot_planes(c->ring_buf, c, which - 2);
   const size_t ly = (size_t)c->wa * c->ha, lc = ly / 4;
   if (y) CK(hipMemcpy(y, p.y, ly * 2, hipMemcpyDeviceToHost));
   if (u) CK(hipMemcpy(u, p.u, lc * 2, hipMemcpyDeviceToHost));
@@ -410,27 +473,32 @@ int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16
 int cairo_ctx_read_inter(cairo_ctx* c, uint8_t* descs, int32_t* sads) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->ks));
-  const size_t n = (size_t)c->wmb * c->hmb * (c->ring > 1 ? c->ring - 1 : 0);
+  int r = sync_all(c);
+  if (r) return r;
+  if (c->last_slot < 0) return kInvalidResource;
+  const size_t n = c->mbs * (c->ring > 1 ? c->ring - 1 : 0);
   if (!n) return kSuccess;
-  if (descs) CK(hipMemcpy(descs, c->inter_desc, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
-  if (sads) CK(hipMemcpy(sads, c->inter_sad, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  const size_t o = (size_t)c->last_slot * c->nref * c->mbs;
+  if (descs) CK(hipMemcpy(descs, c->idesc + o, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
+  if (sads) CK(hipMemcpy(sads, c->isad + o, n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return kSuccess;
 }
 
 int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
   if (!c) return kInvalidArg;
   CK(hipSetDevice(c->device));
+  int r = flush(c);
+  if (r) return r;
   if ((flags & 1) && !c->predeblock) CK(hipMalloc(&c->predeblock, c->plane_elems * 2));
-  if ((flags & 2) && !c->stamps)
-    CK(hipMalloc(&c->stamps, stamp_words(c) * sizeof(uint64_t)));
+  if ((flags & 2) && !c->stamps) CK(hipMalloc(&c->stamps, stamp_words(c) * sizeof(uint64_t)));
   return kSuccess;
 }
 
 int cairo_ctx_read_stamps(cairo_ctx* c, uint64_t* out) {
   if (!c || !c->stamps || !out) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->ks));
+  int r = sync_all(c);
+  if (r) return r;
   CK(hipMemcpy(out, c->stamps, stamp_words(c) * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return kSuccess;
 }
@@ -438,7 +506,8 @@ int cairo_ctx_read_stamps(cairo_ctx* c, uint64_t* out) {
 int cairo_ctx_read_predeblock(cairo_ctx* c, int16_t* y, int16_t* u, int16_t* v) {
   if (!c || !c->predeblock) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->ks));
+  int r = sync_all(c);
+  if (r) return r;
   PlaneSet p = planes_at(c->predeblock, c);
   const size_t ly = (size_t)c->wa * c->ha, lc = ly / 4;
   if (y) CK(hipMemcpy(y, p.y, ly * 2, hipMemcpyDeviceToHost));
@@ -450,8 +519,10 @@ int cairo_ctx_read_predeblock(cairo_ctx* c, int16_t* y, int16_t* u, int16_t* v) 
 int cairo_ctx_read_table(cairo_ctx* c, uint8_t* table) {
   if (!c || !table) return kInvalidArg;
   CK(hipSetDevice(c->device));
-  CK(hipStreamSynchronize(c->ks));
-  CK(hipMemcpy(table, c->table, (size_t)c->wmb * c->hmb * sizeof(BlockDesc),
+  int r = sync_all(c);
+  if (r) return r;
+  if (c->last_slot < 0) return kInvalidResource;
+  CK(hipMemcpy(table, c->table + (size_t)c->last_slot * c->mbs, c->mbs * sizeof(BlockDesc),
                hipMemcpyDeviceToHost));
   return kSuccess;
 }

@@ -15,7 +15,7 @@ struct PlaneSet {
   int16_t* v;
 };
 
-// Plane set of ring slot k inside one contiguous allocation.
+// Plane set k inside one contiguous allocation of plane sets.
 __host__ __device__ inline PlaneSet ring_slot(int16_t* base, size_t slot_elems, int wa, int ha,
                                               int k) {
   PlaneSet p;
@@ -25,63 +25,99 @@ __host__ __device__ inline PlaneSet ring_slot(int16_t* base, size_t slot_elems, 
   return p;
 }
 
-// Per-frame kernel arguments (passed by value).
-struct FrameArgs {
-  int wa, ha;          // frame size aligned to 16 (evx1enc.cpp:79-80)
-  int w, h;            // nominal frame size (RGB input)
-  int wmb, hmb;        // macroblocks per row / column
-  int ring;            // R = ring size (EVX_REFERENCE_FRAME_COUNT)
-  int index;           // frame index (common.cpp:192-195 ring addressing)
-  int inter;           // frame type: 0 intra, 1 inter
-  int quality;         // frame quality 1..31
-  const uint8_t* rgb;  // RGB888, pitch 3*w
-  PlaneSet in;         // input_cache
-  PlaneSet coef;       // output_cache (quantized coefficients, persistent)
-  int16_t* ring_base;       // R contiguous plane sets (Y, U, V each), slot k at
-  size_t slot_elems;        //   ring_base + k * slot_elems
-  BlockDesc* table;        // block table [wmb*hmb]
-  BlockDesc* inter_desc;   // [(off-1)*mbs + mb]
-  int32_t* inter_sad;      // [(off-1)*mbs + mb]
-  int32_t* sync;           // SyncLayout words, zeroed before every frame
-  int32_t* sticky;         // timeout flag that is never cleared (reported by the host)
-  uint64_t* stamps;        // diagnostic: per-MB phase timestamps (nullptr = off)
-  uint64_t* granules;      // K2 hand-off: 192 {tag, 2 px} granules per macroblock
-  uint32_t epoch;          // granule tag of this frame (per-context submission count)
-  int row_workers;         // k_mb_rows: workgroups [0, row_workers) code rows, the rest deblock
-};
-
 // Granule hand-off of a reconstructed macroblock (MI355X_MICROARCH.md, R2 form):
-// 8-byte {high: tag = FrameArgs::epoch, low: two int16 pixels}, each written by
+// 8-byte {high: tag = frame epoch, low: two int16 pixels}, each written by
 // ONE sc1 store; the reader polls the data itself.  Layout per macroblock:
 // 128 luma dwords (row r, pair d at r*8+d), then 32 U and 32 V (row r, pair d
 // at r*4+d).
 constexpr int kGranulesPerMB = 192;
 
-// Phase boundaries recorded per macroblock by k_mb_rows when stamps != nullptr.
+// Phase boundaries recorded per macroblock by the row code when stamps != nullptr.
 constexpr int kStampPhases = 12;  // 10 real-time stamps + 2 shader-clock stamps
-// ...followed by kDbStamps per MB row: deblock worker phases 0..7, and 8 = the
-// row worker's "row coded" publish.
+// ...followed by kDbStamps per MB row: deblock phases 0..7, and 8 = the row
+// coder's "row coded" publish; then 2 words: engine entry (min) / exit (max).
 constexpr int kDbStamps = 9;
 
-// Words of FrameArgs::sync (all int32, zeroed per frame).
-struct SyncLayout {
-  static constexpr int kErr = 0;         // nonzero: a bounded wait timed out
-  static constexpr int kRowTicket = 1;   // K2 row dequeue
-  static constexpr int kDbTicket = 2;    // deblock row dequeue
-  static constexpr int kRowCoded = 8;    // [hmb]: MB row r coded (release/acquire)
-  __host__ __device__ static int deblocked(int hmb) { return kRowCoded + hmb; }  // [hmb]
-  __host__ __device__ static int words(int hmb) { return kRowCoded + 2 * hmb + 8; }
+// Frames per engine launch.
+constexpr int kMaxBatch = 16;
+
+// One frame of a batch (host-filled, kernarg).
+struct FrameDesc {
+  const uint8_t* rgb;  // RGB888, pitch 3*w (device memory)
+  int index;           // frame index (common.cpp:192-195 ring addressing)
+  int inter;           // 0 intra, 1 inter (references 1..R-1)
+  int quality;         // 1..31
+  uint32_t epoch;      // granule tag (per-context submission count, never 0)
+  int slot;            // staging slot: this frame's source / coefficient / table / granule buffers
+  int prev_slot;       // staging slot of the previous frame (output_cache chain)
 };
 
-// Deblock workers appended to the row workers of k_mb_rows.
-constexpr int kDeblockWorkers = 4;
+// Per-frame view of the engine's state (built on the device from EngineArgs).
+struct FrameArgs {
+  int wa, ha;          // frame size aligned to 16 (evx1enc.cpp:79-80)
+  int w, h;            // nominal frame size (RGB input)
+  int wmb, hmb;        // macroblocks per row / column
+  int ring;            // R = ring size (EVX_REFERENCE_FRAME_COUNT)
+  int index, inter, quality;
+  uint32_t epoch;
+  PlaneSet in;         // input_cache of this frame
+  PlaneSet coef;       // output_cache of this frame (persistent semantics: copy MBs carry coef_prev)
+  PlaneSet coef_prev;  // output_cache of the previous frame
+  int16_t* ring_base;  // R contiguous reconstruction slots
+  size_t slot_elems;
+  BlockDesc* table;    // [wmb*hmb]
+  BlockDesc* inter_desc;  // [(off-1)*mbs + mb]
+  int32_t* inter_sad;     // [(off-1)*mbs + mb]
+  uint64_t* granules;  // [mbs * kGranulesPerMB]
+  int32_t* err;        // batch error word (a bounded wait timed out)
+  int32_t* sticky;     // timeout flag that is never cleared (reported by the host)
+  int32_t* inter_done; // [hmb] inter-search tasks finished per MB row
+  int32_t* coded;      // [hmb] MB row coded (slot + table + coefficients written)
+  int32_t* deblocked;  // [hmb] MB row deblocked
+  uint64_t* stamps;    // diagnostic (nullptr = off)
+};
 
-hipError_t launch_convert(const FrameArgs& a, hipStream_t s);
-hipError_t launch_inter_search(const FrameArgs& a, hipStream_t s);
-hipError_t launch_mb_rows(const FrameArgs& a, int workgroups, hipStream_t s);
-// Debug: rebuild the pre-deblock reconstruction of the last frame from the
-// K2 granules into plane set dst.
-hipError_t launch_unpack_granules(const FrameArgs& a, PlaneSet dst, hipStream_t s);
+// Words of the batch sync area (int32, zeroed per batch).
+struct SyncLayout {
+  static constexpr int kErr = 0;
+  static constexpr int kTicketInter = 1;
+  static constexpr int kTicketRows = 2;
+  static constexpr int kTicketDeblock = 3;
+  static constexpr int kFlags = 8;  // then per frame j: inter_done, coded, deblocked [hmb each]
+  __host__ __device__ static int inter_done(int hmb, int j) { return kFlags + 3 * hmb * j; }
+  __host__ __device__ static int coded(int hmb, int j) { return kFlags + 3 * hmb * j + hmb; }
+  __host__ __device__ static int deblocked(int hmb, int j) { return kFlags + 3 * hmb * j + 2 * hmb; }
+  __host__ __device__ static int words(int hmb) { return kFlags + 3 * hmb * kMaxBatch + 8; }
+};
+
+// One engine launch: up to kMaxBatch consecutive frames, pipelined.
+struct EngineArgs {
+  int wa, ha, w, h, wmb, hmb, ring;
+  int nframes;
+  FrameDesc fr[kMaxBatch];
+  // per-slot buffers: base + slot * stride
+  int16_t* src_base;    // plane sets, stride plane_elems
+  int16_t* coef_base;   // plane sets, stride plane_elems
+  size_t plane_elems;
+  BlockDesc* table_base;   // stride mbs
+  BlockDesc* idesc_base;   // stride nref * mbs
+  int32_t* isad_base;      // stride nref * mbs
+  uint64_t* gran_base;     // stride mbs * kGranulesPerMB
+  int16_t* ring_base;      // R reconstruction slots, stride plane_elems
+  int32_t* sync;           // SyncLayout words
+  int32_t* sticky;
+  uint64_t* stamps;
+  int n_inter, n_rows, n_deblock;  // worker pools (workgroups), in blockIdx order
+};
+
+// RGB -> YUV of every frame of the batch into its slot's source planes.
+hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);
+// The pipelined encode engine: inter search, macroblock rows (intra search,
+// classify, transform, quantize, reconstruct) and in-loop deblock.
+hipError_t launch_engine(const EngineArgs& e, hipStream_t s);
+// Debug: rebuild the pre-deblock reconstruction of frame j of the batch from
+// its granules into plane set dst.
+hipError_t launch_unpack_granules(const EngineArgs& e, int j, PlaneSet dst, hipStream_t s);
 
 // Known-answer entry points: apply the device transform / quantizer code to
 // a batch of macroblocks (6 blocks of 64 int16 each, block-major).

@@ -173,15 +173,17 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
 // K0: RGB888 -> YUV 4:2:0 int16 (convert.cpp:11-14, 30-73, 95-160)
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_convert(FrameArgs a) {
-  int qx = blockIdx.x * 256 + threadIdx.x;  // quad column
-  int qy = blockIdx.y;                      // quad row
-  if (qx >= (a.w >> 1)) return;
+__global__ __launch_bounds__(256) void k_convert_batch(EngineArgs e) {
+  const FrameDesc& f = e.fr[blockIdx.z];
+  const int qx = blockIdx.x * 256 + threadIdx.x;  // quad column
+  const int qy = blockIdx.y;                      // quad row
+  if (qx >= (e.w >> 1)) return;
+  const PlaneSet in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
   int su = 0, sv = 0;
 #pragma unroll
   for (int dy = 0; dy < 2; dy++) {
-    const uint8_t* p = a.rgb + ((size_t)(2 * qy + dy) * a.w + 2 * qx) * 3;
-    int16_t* y = a.in.y + (size_t)(2 * qy + dy) * a.wa + 2 * qx;
+    const uint8_t* p = f.rgb + ((size_t)(2 * qy + dy) * e.w + 2 * qx) * 3;
+    int16_t* y = in.y + (size_t)(2 * qy + dy) * e.wa + 2 * qx;
 #pragma unroll
     for (int dx = 0; dx < 2; dx++) {
       int r = p[3 * dx], g = p[3 * dx + 1], b = p[3 * dx + 2];
@@ -190,23 +192,25 @@ __global__ __launch_bounds__(256) void k_convert(FrameArgs a) {
       sv = (int16_t)(sv + (((128 * r - 107 * g - 21 * b + 128) / 256) + 128));
     }
   }
-  a.in.u[(size_t)qy * (a.wa >> 1) + qx] = (int16_t)((su + 2) >> 2);
-  a.in.v[(size_t)qy * (a.wa >> 1) + qx] = (int16_t)((sv + 2) >> 2);
+  in.u[(size_t)qy * (e.wa >> 1) + qx] = (int16_t)((su + 2) >> 2);
+  in.v[(size_t)qy * (e.wa >> 1) + qx] = (int16_t)((sv + 2) >> 2);
 }
 
-hipError_t launch_convert(const FrameArgs& a, hipStream_t s) {
-  dim3 grid((a.w / 2 + 255) / 256, a.h / 2);
-  hipLaunchKernelGGL(k_convert, grid, dim3(256), 0, s, a);
+hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s) {
+  dim3 grid((e.w / 2 + 255) / 256, e.h / 2, e.nframes);
+  hipLaunchKernelGGL(k_convert_batch, grid, dim3(256), 0, s, e);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// Search window in LDS: an 80x80 luma tile and two 40x40 chroma tiles around
-// the macroblock, covering every candidate a search can reach.
+// Inter-search window in LDS, shared by the 4 waves of a workgroup that search
+// 4 horizontally adjacent macroblocks: 80 luma rows x 128 columns (origin 32 px
+// left of / above the first macroblock) and 40 x 64 per chroma plane, covering
+// every candidate the searches can reach.
 // ---------------------------------------------------------------------------
 
-constexpr int kWinL = 80, kWinLP = 88;  // luma tile, pitch (elements)
-constexpr int kWinC = 40, kWinCP = 48;  // chroma tile, pitch (elements)
+constexpr int kWinL = 80, kWinLW = 128, kWinLP = 136;  // luma rows, width, pitch (elements)
+constexpr int kWinC = 40, kWinCW = 64, kWinCP = 72;    // chroma
 
 struct alignas(16) Window {
   int16_t y[kWinL * kWinLP];
@@ -215,22 +219,20 @@ struct alignas(16) Window {
 };
 
 // Stage the in-frame part of the window with origin (ox, oy) (luma pixels,
-// multiples of 16) from plane set p.  All threads of the block participate.
+// multiples of 16) from plane set p.  All 256 threads participate.
 __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa, int ha, int ox,
-                                            int oy, int nthreads) {
-  // Luma: 80 rows x 10 chunks of 8 pixels (16 B).
-  for (int k = threadIdx.x; k < kWinL * 10; k += nthreads) {
-    int r = k / 10, c = (k - r * 10) * 8;
-    int gy = oy + r, gx = ox + c;
+                                            int oy) {
+  for (int k = threadIdx.x; k < kWinL * (kWinLW / 8); k += 256) {  // 16-B chunks
+    const int r = k >> 4, c = (k & 15) * 8;
+    const int gy = oy + r, gx = ox + c;
     if (gy >= 0 && gy < ha && gx >= 0 && gx < wa)
       *(int4*)&w.y[r * kWinLP + c] = *(const int4*)&p.y[(size_t)gy * wa + gx];
   }
-  // Chroma: 40 rows x 5 chunks of 8 pixels, per plane.
-  int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
-  for (int k = threadIdx.x; k < 2 * kWinC * 5; k += nthreads) {
-    int pl = k / (kWinC * 5), kk = k - pl * kWinC * 5;
-    int r = kk / 5, c = (kk - r * 5) * 8;
-    int gy = coy + r, gx = cox + c;
+  const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
+  for (int k = threadIdx.x; k < 2 * kWinC * (kWinCW / 8); k += 256) {
+    const int pl = k / (kWinC * 8), kk = k - pl * kWinC * 8;
+    const int r = kk >> 3, c = (kk & 7) * 8;
+    const int gy = coy + r, gx = cox + c;
     if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
       const int16_t* src = pl ? p.v : p.u;
       int16_t* dst = pl ? w.v : w.u;
@@ -440,73 +442,85 @@ __device__ __forceinline__ BlockDesc make_desc(const Sel& s, int px, int py, int
 }
 
 // ---------------------------------------------------------------------------
-// K1: inter search, one wave64 per (macroblock, reference offset)
-// (calculate_inter_prediction, motion.cpp:421-494)
+// Inter search task (calculate_inter_prediction, motion.cpp:421-494): one
+// workgroup searches macroblocks 4g..4g+3 of row r against reference offset
+// `off`, one wave per macroblock, in the shared window.
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(64) void k_inter_search(FrameArgs a) {
-  __shared__ Window win;
-  const int mbs = a.wmb * a.hmb, nref = a.ring - 1;
-  const int task = xcd_remap(blockIdx.x, mbs * nref);
-  if (task < 0) return;
-  const int off = task / mbs + 1, mb = task - (off - 1) * mbs;
-  const int px = (mb % a.wmb) * kMB, py = (mb / a.wmb) * kMB;
+struct InterLds {
+  Window win;
+  int need[4];
+};
+
+__device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int off, InterLds& L) {
+  const int wave = threadIdx.x >> 6;
+  const int x = 4 * g + wave;
+  const bool valid = x < a.wmb;
+  const int px = x * kMB, py = r * kMB, mb = r * a.wmb + x;
+  const int mbs = a.wmb * a.hmb;
   const int thr = (a.quality >> 2) + 1;
   const PlaneSet ref = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, (a.index + a.ring - off) % a.ring);
-
-  const Px6 src = px_from_planes(a.in, a.wa, px, py);
   Sel s;
+  Px6 src;
   s.bx = px;
   s.by = py;
   s.ssd = INT32_MAX;
   s.sp_idx = s.sp_amt = s.sp_en = 0;
-  sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
-
-  if (s.mad >= thr) {
-    const int ox = px - 32, oy = py - 32;  // window origin
-    load_window(win, ref, a.wa, a.ha, ox, oy, 64);
+  s.sad = s.mad = 0;
+  if (valid) {  // zero-MV candidate straight from the planes
+    src = px_from_planes(a.in, a.wa, px, py);
+    sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
+  }
+  const bool need = valid && s.mad >= thr;
+  if ((threadIdx.x & 63) == 0) L.need[wave] = need;
+  __syncthreads();
+  if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
+    const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
+    load_window(L.win, ref, a.wa, a.ha, ox, oy);
     __syncthreads();
-    for (int step = kRadius; step > 0; step >>= 1) {
+    if (need) {
+      for (int step = kRadius; step > 0; step >>= 1) {
+        const int bx = s.bx, by = s.by;
+        for (int j = -step; j <= step; j += step)
+          for (int i = -step; i <= step; i += step) {
+            const int cx = bx + i, cy = by + j;
+            if (!in_frame(cx, cy, a.wa, a.ha)) continue;
+            int sad, mad;
+            sad_mad(src, px_from_window(L.win, cx - ox, cy - oy), sad, mad);
+            accept_int(s, cx, cy, sad, mad, px, py, thr);
+          }
+      }
+      // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
+      const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
+      s.sp_idx = s.sp_amt = s.sp_en = 0;
       const int bx = s.bx, by = s.by;
-      for (int j = -step; j <= step; j += step)
-        for (int i = -step; i <= step; i += step) {
-          const int cx = bx + i, cy = by + j;
-          if (!in_frame(cx, cy, a.wa, a.ha)) continue;
-          int sad, mad;
-          sad_mad(src, px_from_window(win, cx - ox, cy - oy), sad, mad);
-          accept_int(s, cx, cy, sad, mad, px, py, thr);
+      for (int j = -1; j <= 1; j++)
+        for (int i = -1; i <= 1; i++) {
+          if (i == 0 && j == 0) continue;
+          const int tx = bx + i, ty = by + j;
+          if (!in_frame(tx, ty, a.wa, a.ha)) continue;
+          const Px6 nb = px_from_window(L.win, tx - ox, ty - oy);
+          const int idx = frac_index(i, j);
+          for (int q = 0; q < 2; q++) {
+            int sad, mad;
+            sad_mad(src, lerp6(best, nb, q), sad, mad);
+            accept_sub(s, idx, q, sad, mad, thr);
+          }
         }
     }
-    // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
-    const Px6 best = px_from_window(win, s.bx - ox, s.by - oy);
-    s.sp_idx = s.sp_amt = s.sp_en = 0;
-    const int bx = s.bx, by = s.by;
-    for (int j = -1; j <= 1; j++)
-      for (int i = -1; i <= 1; i++) {
-        if (i == 0 && j == 0) continue;
-        const int tx = bx + i, ty = by + j;
-        if (!in_frame(tx, ty, a.wa, a.ha)) continue;
-        const Px6 nb = px_from_window(win, tx - ox, ty - oy);
-        const int idx = frac_index(i, j);
-        for (int q = 0; q < 2; q++) {
-          int sad, mad;
-          sad_mad(src, lerp6(best, nb, q), sad, mad);
-          accept_sub(s, idx, q, sad, mad, thr);
-        }
-      }
   }
+  if (valid && (threadIdx.x & 63) == 0) {
+    a.inter_desc[(off - 1) * mbs + mb] = make_desc(s, px, py, thr, false, off);
+    a.inter_sad[(off - 1) * mbs + mb] = s.sad;
+  }
+  // all records of this task stored; release them to the row coder
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
-    a.inter_desc[task] = make_desc(s, px, py, thr, false, off);
-    a.inter_sad[task] = s.sad;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(&a.inter_done[r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-hipError_t launch_inter_search(const FrameArgs& a, hipStream_t s) {
-  int n = a.wmb * a.hmb * (a.ring - 1);
-  if (n <= 0) return hipSuccess;
-  int grid = ((n + 7) / 8) * 8;
-  hipLaunchKernelGGL(k_inter_search, dim3(grid), dim3(64), 0, s, a);
-  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -753,60 +767,53 @@ __device__ __forceinline__ void db_v(int16_t* img, int width, int mbsz, int j, b
                     });
 }
 
-// Deblock worker: MB rows in order, each once row r is coded and row r-1 is
-// filtered.  Row workers never wait on deblock workers (no deadlock).
+// Deblock MB row r of frame a once row r is coded and row r-1 is filtered
+// (whole workgroup).  The row coders never wait on the deblock (no deadlock).
 // dq: LDS scratch of 2 * wmb int16.
-__device__ __forceinline__ void deblock_rows(const FrameArgs& a, int16_t* dq, int* slot) {
+__device__ __forceinline__ void deblock_task(const FrameArgs& a, int r, int16_t* dq) {
   const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
-  int32_t* err = a.sync + SyncLayout::kErr;
-  int32_t* coded = a.sync + SyncLayout::kRowCoded;
-  int32_t* done = a.sync + SyncLayout::deblocked(a.hmb);
   const int cw = a.wa >> 1;
-  for (;;) {
-    const int r = dequeue(a.sync + SyncLayout::kDbTicket, slot);
-    if (r >= a.hmb) break;
-    uint64_t* ds = a.stamps ? a.stamps + (size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps : nullptr;
+  uint64_t* ds = a.stamps ? a.stamps + (size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps : nullptr;
 #define DB_STAMP(k) \
   if (ds && threadIdx.x == 0) ds[k] = __builtin_amdgcn_s_memrealtime();
-    DB_STAMP(0);
-    if (threadIdx.x == 0) {
-      wait_at_least(&coded[r], 1, err, a.sticky);
-      if (r > 0) wait_at_least(&done[r - 1], 1, err, a.sticky);
-    }
-    DB_STAMP(1);
-    acquire_after_wait();
-    DB_STAMP(2);
-    for (int i = threadIdx.x; i < 2 * a.wmb; i += 256) {
-      const int row = r - 1 + (i >= a.wmb), col = i >= a.wmb ? i - a.wmb : i;
-      int e = 0;
-      if (row >= 0) {
-        const BlockDesc& d = a.table[row * a.wmb + col];
-        e = ((d.block_type & kCopy) ? 0x100 : 0) | d.q_index;
-      }
-      dq[i] = (int16_t)e;
-    }
-    __syncthreads();
-    DB_STAMP(3);
-    if (r > 0) {  // band 2r (luma) / r (chroma): top edges, then vertical edges
-      db_h(cs.y, a.wa, 16, 16 * r, true, dq, false);
-      db_h(cs.u, cw, 8, 8 * r, false, dq, false);
-      db_h(cs.v, cw, 8, 8 * r, false, dq, false);
-    }
-    __syncthreads();
-    DB_STAMP(4);
-    db_v(cs.y, a.wa, 16, 16 * r, true, dq);
-    db_v(cs.u, cw, 8, 8 * r, false, dq);
-    db_v(cs.v, cw, 8, 8 * r, false, dq);
-    __syncthreads();
-    DB_STAMP(5);
-    db_h(cs.y, a.wa, 16, 16 * r + 8, true, dq, true);  // band 2r+1: MB-interior edge
-    __syncthreads();
-    DB_STAMP(6);
-    db_v(cs.y, a.wa, 16, 16 * r + 8, true, dq);
-    publish(&done[r], 1);
-    DB_STAMP(7);
-#undef DB_STAMP
+  DB_STAMP(0);
+  if (threadIdx.x == 0) {
+    wait_at_least(&a.coded[r], 1, a.err, a.sticky);
+    if (r > 0) wait_at_least(&a.deblocked[r - 1], 1, a.err, a.sticky);
   }
+  DB_STAMP(1);
+  acquire_after_wait();
+  DB_STAMP(2);
+  for (int i = threadIdx.x; i < 2 * a.wmb; i += 256) {
+    const int row = r - 1 + (i >= a.wmb), col = i >= a.wmb ? i - a.wmb : i;
+    int e = 0;
+    if (row >= 0) {
+      const BlockDesc& d = a.table[row * a.wmb + col];
+      e = ((d.block_type & kCopy) ? 0x100 : 0) | d.q_index;
+    }
+    dq[i] = (int16_t)e;
+  }
+  __syncthreads();
+  DB_STAMP(3);
+  if (r > 0) {  // band 2r (luma) / r (chroma): top edges, then vertical edges
+    db_h(cs.y, a.wa, 16, 16 * r, true, dq, false);
+    db_h(cs.u, cw, 8, 8 * r, false, dq, false);
+    db_h(cs.v, cw, 8, 8 * r, false, dq, false);
+  }
+  __syncthreads();
+  DB_STAMP(4);
+  db_v(cs.y, a.wa, 16, 16 * r, true, dq);
+  db_v(cs.u, cw, 8, 8 * r, false, dq);
+  db_v(cs.v, cw, 8, 8 * r, false, dq);
+  __syncthreads();
+  DB_STAMP(5);
+  db_h(cs.y, a.wa, 16, 16 * r + 8, true, dq, true);  // band 2r+1: MB-interior edge
+  __syncthreads();
+  DB_STAMP(6);
+  db_v(cs.y, a.wa, 16, 16 * r + 8, true, dq);
+  publish(&a.deblocked[r], 1);
+  DB_STAMP(7);
+#undef DB_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -840,7 +847,6 @@ struct alignas(16) RowLds {
   int16_t bufA[kMBElems], bufB[kMBElems];  // per-block transform scratch, block-major
   int32_t cand[2][16][2];                  // double-buffered candidate (sad, mad)
   int32_t red[12];
-  int slot;
 };
 
 // Dword k (0..191) of macroblock (mbx, mby): its address in plane set p and in
@@ -981,31 +987,19 @@ __device__ __forceinline__ uint64_t* gran_at(const FrameArgs& a, int mbx, int mb
   return a.granules + (size_t)(mby * a.wmb + mbx) * kGranulesPerMB + k;
 }
 
-__global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
-  __shared__ RowLds L;
+// Code MB row `by` of frame a (intra search, classify, transform, VAQ,
+// quantize, reconstruct), left to right; whole workgroup.
+__device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
   const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
-  int32_t* err = a.sync + SyncLayout::kErr;
+  int32_t* err = a.err;
   const uint32_t tag = a.epoch;
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
   const int mbs = a.wmb * a.hmb;
-  uint64_t* ks = a.stamps ? a.stamps + (size_t)mbs * kStampPhases + (size_t)a.hmb * kDbStamps : nullptr;
-  if (ks && tid == 0) {  // kernel entry (min) / exit (max) over workgroups
-    __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if ((int)blockIdx.x >= a.row_workers) {  // in-loop deblock workers
-    deblock_rows(a, L.win.y, &L.slot);
-    if (ks && tid == 0)
-      __hip_atomic_fetch_max(&ks[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-
-  for (;;) {
-    const int by = dequeue(a.sync + SyncLayout::kRowTicket, &L.slot);
-    if (by >= a.hmb) break;
+  {
     const int py = by * kMB, oy = py - 48;
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
@@ -1212,9 +1206,17 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
                                   dequant_elem(e, qv, qp, intra_path));
           pv[bi] = (int16_t)(has_pred ? t + pv[bi] : t);  // reconstruction (unclamped)
         }
-      } else {
+      } else {  // copy: output_cache keeps this macroblock's previous coefficients
         d.q_index = 0;
         d.variance = 0;
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+          const int e = (wave + 4 * bi) * 64 + lane;
+          int pl, ex, ey;
+          elem_coords(e, px, py, pl, ex, ey);
+          const size_t o = (size_t)ey * (pl ? cw : a.wa) + ex;
+          (pl == 0 ? a.coef.y : (pl == 1 ? a.coef.u : a.coef.v))[o] =
+              (pl == 0 ? a.coef_prev.y : (pl == 1 ? a.coef_prev.u : a.coef_prev.v))[o];
+        }
       }
       stamp(a, mb, 7);
       // reconstruction -> current slot (global) and the window
@@ -1254,15 +1256,123 @@ __global__ __launch_bounds__(256) void k_mb_rows(FrameArgs a) {
       stamp(a, mb, 9);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
-    publish(&a.sync[SyncLayout::kRowCoded + by], 1);  // row by coded: the deblock may start
+    publish(&a.coded[by], 1);  // row by coded: the deblock and later frames may use it
     if (a.stamps && tid == 0)
       a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)by * kDbStamps + 8] = __builtin_amdgcn_s_memrealtime();
   }
-  if (ks && tid == 0)
+}
+
+__device__ __forceinline__ FrameArgs frame_view(const EngineArgs& e, int j) {
+  const FrameDesc& f = e.fr[j];
+  FrameArgs a;
+  a.wa = e.wa, a.ha = e.ha, a.w = e.w, a.h = e.h, a.wmb = e.wmb, a.hmb = e.hmb, a.ring = e.ring;
+  a.index = f.index;
+  a.inter = f.inter && e.ring > 1;
+  a.quality = f.quality;
+  a.epoch = f.epoch;
+  a.in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
+  a.coef = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.slot);
+  a.coef_prev = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.prev_slot);
+  a.ring_base = e.ring_base;
+  a.slot_elems = e.plane_elems;
+  const size_t mbs = (size_t)e.wmb * e.hmb, nref = e.ring > 1 ? e.ring - 1 : 1;
+  a.table = e.table_base + (size_t)f.slot * mbs;
+  a.inter_desc = e.idesc_base + (size_t)f.slot * nref * mbs;
+  a.inter_sad = e.isad_base + (size_t)f.slot * nref * mbs;
+  a.granules = e.gran_base + (size_t)f.slot * mbs * kGranulesPerMB;
+  a.err = e.sync + SyncLayout::kErr;
+  a.sticky = e.sticky;
+  a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, j);
+  a.coded = e.sync + SyncLayout::coded(e.hmb, j);
+  a.deblocked = e.sync + SyncLayout::deblocked(e.hmb, j);
+  a.stamps = e.stamps;
+  return a;
+}
+
+struct EngineLds {
+  union {
+    RowLds row;
+    InterLds inter;
+  } u;
+  int slot;
+};
+
+// ---------------------------------------------------------------------------
+// The engine: one persistent launch encodes a batch of consecutive frames,
+// pipelined across frames.  Three worker pools (blockIdx ranges) dequeue
+// their tasks in (frame, row) order:
+//   inter    (j, r, g, off): inter search of MBs 4g..4g+3 of row r against
+//            reference offset off; needs the batch's references deblocked
+//            through MB row r+3 (the search reaches 47 rows below the row top,
+//            and the next row's deblock rewrites 3 of them);
+//   rows     (j, r): code MB row r; needs the row's inter records, the frames
+//            still reading this slot's previous content (j-1..j-R+1) coded
+//            through row r+2, and the stale rows below final (frame j-R
+//            deblocked through row r+2); rows above arrive as granules;
+//   deblock  (j, r): needs row r coded and row r-1 deblocked.
+// Every wait targets an earlier frame or an earlier stage/row of the same
+// frame, and each pool dequeues in order, so the oldest unfinished task is
+// always running: no deadlock with every workgroup resident.
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_engine(EngineArgs e) {
+  __shared__ EngineLds L;
+  const int b = blockIdx.x, hmb = e.hmb;
+  const int nref = e.ring > 1 ? e.ring - 1 : 0;
+  int32_t* err = e.sync + SyncLayout::kErr;
+  uint64_t* ks = e.stamps ? e.stamps + (size_t)e.wmb * hmb * kStampPhases + (size_t)hmb * kDbStamps : nullptr;
+  if (ks && threadIdx.x == 0)
+    __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ng = (e.wmb + 3) >> 2;
+  if (b < e.n_inter) {
+    const int per_row = ng * nref, per_frame = hmb * per_row;
+    const int total = e.nframes * per_frame;
+    for (;;) {
+      const int t = dequeue(e.sync + SyncLayout::kTicketInter, &L.slot);
+      if (t >= total) break;
+      const int j = t / per_frame, rem = t - j * per_frame, r = rem / per_row;
+      const int rem2 = rem - r * per_row, g = rem2 / nref, off = rem2 - g * nref + 1;
+      const FrameArgs a = frame_view(e, j);
+      if (!a.inter) continue;
+      if (threadIdx.x == 0)
+        for (int o = 1; o <= nref && j - o >= 0; o++)
+          wait_at_least(e.sync + SyncLayout::deblocked(hmb, j - o) + min(r + 3, hmb - 1), 1, err, e.sticky);
+      acquire_after_wait();
+      inter_task(a, r, g, off, L.u.inter);
+    }
+  } else if (b < e.n_inter + e.n_rows) {
+    const int total = e.nframes * hmb;
+    for (;;) {
+      const int t = dequeue(e.sync + SyncLayout::kTicketRows, &L.slot);
+      if (t >= total) break;
+      const int j = t / hmb, r = t - j * hmb;
+      const FrameArgs a = frame_view(e, j);
+      if (threadIdx.x == 0) {
+        if (a.inter) wait_at_least(&a.inter_done[r], ng * nref, err, e.sticky);
+        for (int o = 1; o < e.ring && j - o >= 0; o++)
+          wait_at_least(e.sync + SyncLayout::coded(hmb, j - o) + min(r + 2, hmb - 1), 1, err, e.sticky);
+        if (j - e.ring >= 0)
+          wait_at_least(e.sync + SyncLayout::deblocked(hmb, j - e.ring) + min(r + 2, hmb - 1), 1, err,
+                        e.sticky);
+      }
+      acquire_after_wait();
+      code_row(a, r, L.u.row);
+    }
+  } else {
+    const int total = e.nframes * hmb;
+    for (;;) {
+      const int t = dequeue(e.sync + SyncLayout::kTicketDeblock, &L.slot);
+      if (t >= total) break;
+      const int j = t / hmb, r = t - j * hmb;
+      deblock_task(frame_view(e, j), r, L.u.row.win.y);
+    }
+  }
+  if (ks && threadIdx.x == 0)
     __hip_atomic_fetch_max(&ks[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(192) void k_unpack_granules(FrameArgs a, PlaneSet dst) {
+__global__ __launch_bounds__(192) void k_unpack_granules(EngineArgs e, int j, PlaneSet dst) {
+  const FrameArgs a = frame_view(e, j);
   const int mb = blockIdx.x, k = threadIdx.x;
   const int mbx = mb % a.wmb, mby = mb / a.wmb;
   const uint32_t v = (uint32_t)a.granules[(size_t)mb * kGranulesPerMB + k];
@@ -1277,17 +1387,13 @@ __global__ __launch_bounds__(192) void k_unpack_granules(FrameArgs a, PlaneSet d
   p[1] = (int16_t)(v >> 16);
 }
 
-hipError_t launch_unpack_granules(const FrameArgs& a, PlaneSet dst, hipStream_t s) {
-  hipLaunchKernelGGL(k_unpack_granules, dim3(a.wmb * a.hmb), dim3(kGranulesPerMB), 0, s, a, dst);
+hipError_t launch_unpack_granules(const EngineArgs& e, int j, PlaneSet dst, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack_granules, dim3(e.wmb * e.hmb), dim3(kGranulesPerMB), 0, s, e, j, dst);
   return hipGetLastError();
 }
 
-hipError_t launch_mb_rows(const FrameArgs& a0, int workgroups, hipStream_t s) {
-  FrameArgs a = a0;
-  int g = workgroups > 0 ? workgroups : a.hmb;
-  if (g > a.hmb) g = a.hmb;
-  a.row_workers = g;
-  hipLaunchKernelGGL(k_mb_rows, dim3(g + kDeblockWorkers), dim3(256), 0, s, a);
+hipError_t launch_engine(const EngineArgs& e, hipStream_t s) {
+  hipLaunchKernelGGL(k_engine, dim3(e.n_inter + e.n_rows + e.n_deblock), dim3(256), 0, s, e);
   return hipGetLastError();
 }
 

@@ -54,20 +54,27 @@ CAIRO_API int cairo_ctx_destroy(cairo_ctx *ctx);
 /* Zero every plane (fresh-encoder state, common.cpp:79-150). */
 CAIRO_API int cairo_ctx_reset(cairo_ctx *ctx);
 
-/* Enqueue the hot path for frame (index, type 0=intra/1=inter, quality).
- * rgb is RGB888 with pitch 3*width, in host memory (rgb_on_device = 0) or
- * device memory of this context's GPU (1).  Returns a ticket. */
+/* Submit frame (index, type 0=intra/1=inter, quality).  rgb is RGB888 with
+ * pitch 3*width, in host memory (rgb_on_device = 0) or device memory of this
+ * context's GPU (1; must stay valid until the frame's wait).  Frames are
+ * encoded in batches of up to cairo_ctx_set_batch frames, pipelined on the GPU
+ * in one launch; a batch launches when full or when a frame of it is waited
+ * on.  Returns a ticket. */
 CAIRO_API int cairo_ctx_submit(cairo_ctx *ctx, const uint8_t *rgb, int rgb_on_device,
                                uint32_t index, uint32_t type, uint32_t quality, int *ticket);
 /* Wait until the frame's block table and coefficients are host-visible. */
 CAIRO_API int cairo_ctx_wait(cairo_ctx *ctx, int ticket, cairo_frame_result *out);
 /* Hand the ticket's staging buffers back (required before ticket+stages). */
 CAIRO_API int cairo_ctx_release(cairo_ctx *ctx, int ticket);
-/* Block until all submitted GPU work (including the deblock) is finished. */
+/* Launch any pending frames and block until all GPU work is finished. */
 CAIRO_API int cairo_ctx_sync(cairo_ctx *ctx);
+/* Staging slots = frames that may be in flight (submitted, not released). */
 CAIRO_API int cairo_ctx_stages(const cairo_ctx *ctx);
+/* Frames per engine launch, 1..stages/2 (default 8). */
+CAIRO_API int cairo_ctx_set_batch(cairo_ctx *ctx, int frames);
 
-/* Introspection (synchronous).  which: 0 input, 1 output_cache, 2+k slot k. */
+/* Introspection (synchronous; of the last submitted frame).  which: 0 input,
+ * 1 output_cache, 2+k ring slot k. */
 CAIRO_API int cairo_ctx_read_planes(cairo_ctx *ctx, int which, int16_t *y, int16_t *u,
                                     int16_t *v);
 /* Inter-search records of the last frame: (ring-1)*mbs descs and SADs. */
@@ -83,11 +90,11 @@ CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, 
 
 /* Per-kernel timing (HIP events on the kernels' stream), opt-in. */
 CAIRO_API int cairo_ctx_set_profiling(cairo_ctx *ctx, int enable);
-/* Accumulated ms per kernel since the last call: [convert, inter search,
- * macroblock rows (coding + in-loop deblock)], and the number of frames they
- * cover; resets the accumulators. */
+/* Accumulated ms per kernel since the last call: [convert, 0 (inter search
+ * runs inside the engine), engine (inter search + row coding + in-loop
+ * deblock)], and the number of frames they cover; resets the accumulators. */
 CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[3], int *frames);
-/* Workgroup count of the macroblock-row kernel (0 = one per MB row). */
+/* Row-coder workgroups of the engine (0 = automatic). */
 CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows);
 
 /* Known-answer check of the device transform chain: count macroblocks of 384

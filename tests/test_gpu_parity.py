@@ -196,3 +196,58 @@ def test_encoder_stream_matches_golden(orc, cairo, cfg):
         hsh = orc.fnv1a64(orc.canonical_frame_bytes(bs.data(), n, t == 0), hsh)
     assert f"{hsh:016x}" == cfg["fnv1a64"]
     enc.close()
+
+
+# ---------------------------------------------------------------------------
+# Pipelined batches: several frames in one engine launch (frames overlap on
+# the GPU with row-level dependencies); every frame must still match.
+# ---------------------------------------------------------------------------
+
+def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0):
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    ref = []
+    for t in range(frames):
+        rgb = orc.make_frame(w, h, t)
+        intra = t == 0 or (intra_every and t % intra_every == 0)
+        if intra:
+            e.insert_intra()
+        e.encode(rgb)
+        ref.append((intra, e.block_table(), e.planes(1)))
+    final_slots = [e.planes(2 + k) for k in range(ring)]
+    ctx = cairo.Context(w, h, ring)
+    ctx.set_batch(batch)
+    tickets = [ctx.submit(orc.make_frame(w, h, t), t, not ref[t][0], q) for t in range(frames)]
+    for t, tk in enumerate(tickets):
+        out = ctx.wait(tk)
+        tag = f"{w}x{h} R={ring} q={q} batch={batch} frame {t}"
+        _table_equal(out.table, ref[t][1], f"{tag}: block table")
+        np.testing.assert_array_equal(out.coef_y, ref[t][2][0], err_msg=f"{tag}: coef Y")
+        np.testing.assert_array_equal(out.coef_u, ref[t][2][1], err_msg=f"{tag}: coef U")
+        np.testing.assert_array_equal(out.coef_v, ref[t][2][2], err_msg=f"{tag}: coef V")
+        ctx.release(tk)
+    ctx.sync()
+    for k in range(ring):
+        gy, gu, gv = ctx.read_planes(2 + k)
+        np.testing.assert_array_equal(gy, final_slots[k][0], err_msg=f"slot {k} Y")
+        np.testing.assert_array_equal(gu, final_slots[k][1], err_msg=f"slot {k} U")
+        np.testing.assert_array_equal(gv, final_slots[k][2], err_msg=f"slot {k} V")
+    ctx.close()
+
+
+@pytest.mark.parametrize("ring,batch", [(2, 8), (4, 8), (3, 5), (2, 1)])
+def test_batched_cif(orc, cairo, ring, batch):
+    _run_batched(orc, cairo, 352, 288, ring, 16, 12, batch)
+
+
+def test_batched_mixed_intra(orc, cairo):
+    _run_batched(orc, cairo, 352, 288, 4, 8, 12, 8, intra_every=3)
+
+
+def test_batched_720p(orc, cairo):
+    _run_batched(orc, cairo, 1280, 720, 2, 16, 10, 8)
+
+
+def test_batched_ragged(orc, cairo):
+    _run_batched(orc, cairo, 200, 120, 3, 16, 9, 4)
+    _run_batched(orc, cairo, 16, 16, 2, 16, 6, 6)
