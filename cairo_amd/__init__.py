@@ -249,13 +249,18 @@ class Context:
         return y, u, v
 
     def read_stamps(self):
-        """-> (per-MB stamps (hmb, wmb, 12), per-row deblock stamps (hmb, 9),
-        kernel [entry, exit]); 100 MHz ticks."""
-        n_mb, n_db = self.hmb * self.wmb * 12, self.hmb * 9
-        out = np.zeros(n_mb + n_db + 2, np.uint64)
+        """-> (per-MB stamps (16, hmb, wmb, 12), per-row deblock chunk stamps (16, hmb, 256),
+        engine [entry, exit], inter-task stamps (16, hmb, ng, nref, 3)) for the
+        frames of the last batch; 100 MHz ticks."""
+        n_mb, n_db = self.hmb * self.wmb * 12, self.hmb * 256
+        fw = n_mb + n_db
+        ng, nref = (self.wmb + 3) // 4, max(self.ring - 1, 1)
+        n_it = 16 * self.hmb * ng * nref * 3
+        out = np.zeros(16 * fw + 2 + n_it, np.uint64)
         _ck(self.L.cairo_ctx_read_stamps(self.h, _ptr(out)), "read_stamps")
-        return (out[:n_mb].reshape(self.hmb, self.wmb, 12), out[n_mb:n_mb + n_db].reshape(self.hmb, 9),
-                out[n_mb + n_db:])
+        fr = out[: 16 * fw].reshape(16, fw)
+        return (fr[:, :n_mb].reshape(16, self.hmb, self.wmb, 12), fr[:, n_mb:].reshape(16, self.hmb, 256),
+                out[16 * fw:16 * fw + 2], out[16 * fw + 2:].reshape(16, self.hmb, ng, nref, 3))
 
     def set_profiling(self, enable: bool) -> None:
         _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")

@@ -67,6 +67,12 @@ struct cairo_ctx {
   uint8_t* rgb = nullptr;
   int16_t* ring_buf = nullptr;
   int32_t *sync = nullptr, *sticky = nullptr;
+  int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
+  FrameArgs* fdesc_host = nullptr;  // pinned [kStages][kMaxBatch]: per-frame views per launch
+  FrameArgs* fdesc = nullptr;       // device copy
+  int fdesc_next = 0;
+  int32_t* trace_host = nullptr;  // diagnostic live trace (mapped), opt-in via set_debug(4)
+  int32_t* trace_dev = nullptr;
   size_t sync_words = 0;
   Stage st[kStages];
   int next_ticket = 0;
@@ -106,7 +112,9 @@ PlaneSet slot_planes(int16_t* base, const cairo_ctx* c, int slot) {
 }
 
 size_t stamp_words(const cairo_ctx* c) {
-  return c->mbs * kStampPhases + (size_t)c->hmb * kDbStamps + 2;
+  // frames, engine entry/exit, then 3 stamps per inter task
+  return kMaxBatch * stamp_frame_words((int)c->wmb, (int)c->hmb) + 2 +
+         (size_t)kMaxBatch * c->hmb * ((c->wmb + 3) / 4) * c->nref * 3;
 }
 
 EngineArgs engine_args(const cairo_ctx* c) {
@@ -125,6 +133,8 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.sync = c->sync;
   e.sticky = c->sticky;
   e.stamps = c->stamps;
+  e.order = c->order;
+  e.trace = c->trace_dev;
   return e;
 }
 
@@ -143,7 +153,9 @@ void free_ctx(cairo_ctx* c) {
     for (auto& e : t.ev)
       if (e) (void)hipEventDestroy(e);
   if (c->engine_done) (void)hipEventDestroy(c->engine_done);
-  for (void* p : {(void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad,
+  if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
+  if (c->trace_host) (void)hipHostFree(c->trace_host);
+  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps})
     (void)hipFree(p);
@@ -158,7 +170,7 @@ int zero_state(cairo_ctx* c) {
   CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
   CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * kStages, c->ks));
   // granule tags start at 0; the n-th submission after a reset publishes tag n
-  CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranulesPerMB * sizeof(uint64_t) * kStages, c->ks));
+  CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * kStages, c->ks));
   CK(hipStreamSynchronize(c->ks));
   c->epoch = 0;
   c->last_slot = -1;
@@ -184,19 +196,28 @@ int flush(cairo_ctx* c) {
   CK(hipSetDevice(c->device));
   EngineArgs e = engine_args(c);
   e.nframes = c->npend;
+  e.order = c->order + (size_t)(e.nframes - 1) * kMaxBatch * c->hmb;
+  // frame descriptors -> device (a ring of pinned slots: the copy of an earlier
+  // launch may still be pending when this one is written)
+  const int fslot = c->fdesc_next;
+  c->fdesc_next = (c->fdesc_next + 1) % kStages;
+  FrameArgs* fh = c->fdesc_host + (size_t)fslot * kMaxBatch;
+  FrameArgs* fd = c->fdesc + (size_t)fslot * kMaxBatch;
   bool any_inter = false;
   for (int i = 0; i < c->npend; i++) {
-    e.fr[i] = c->pend[i];
-    any_inter |= e.fr[i].inter && c->ring > 1;
+    fh[i] = make_frame_view(e, c->pend[i], i);
+    any_inter |= fh[i].inter != 0;
   }
+  e.fa = fd;
   const int rows = e.nframes * e.hmb;
   const int ng = (e.wmb + 3) / 4;
-  e.n_rows = c->wg_rows > 0 ? c->wg_rows : rows;
-  if (e.n_rows > 240) e.n_rows = 240;
+  // Residency: 2 workgroups per CU (VGPRs), 256 CUs.  Every row has a coder
+  // and a helper (inter search + deblock) living as long as the row: equal pools.
+  (void)any_inter;
+  (void)ng;
+  e.n_rows = c->wg_rows > 0 ? c->wg_rows : 240;
   if (e.n_rows > rows) e.n_rows = rows;
-  e.n_inter = any_inter ? rows * ng * (int)c->nref : 0;
-  if (e.n_inter > 64) e.n_inter = 64;
-  e.n_deblock = rows < 8 ? rows : 8;
+  e.n_helpers = e.n_rows;
   TimedBatch* tb = nullptr;
   if (c->profiling) {
     tb = &c->tb[c->tb_next];
@@ -204,10 +225,12 @@ int flush(cairo_ctx* c) {
     int r = collect_times(c, *tb);  // its events are about to be reused
     if (r) return r;
   }
+  CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, c->ks));
   CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t), c->ks));
   if (c->stamps) {  // engine entry (min) / exit (max) words
     static const uint64_t init[2] = {~0ull, 0};
-    CK(hipMemcpyAsync(c->stamps + stamp_words(c) - 2, init, sizeof(init), hipMemcpyHostToDevice, c->ks));
+    CK(hipMemcpyAsync(c->stamps + kMaxBatch * stamp_frame_words((int)c->wmb, (int)c->hmb), init, sizeof(init),
+                      hipMemcpyHostToDevice, c->ks));
   }
   if (tb) CK(hipEventRecord(tb->ev[0], c->ks));
   CK(launch_convert_batch(e, c->ks));
@@ -219,13 +242,13 @@ int flush(cairo_ctx* c) {
     tb->frames = e.nframes;
     tb->pending = true;
   }
-  const int last = e.fr[e.nframes - 1].slot;
+  const int last = c->pend[e.nframes - 1].slot;
   if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), c->ks));
   // outputs for the host entropy stage, on the copy stream
   CK(hipEventRecord(c->engine_done, c->ks));
   CK(hipStreamWaitEvent(c->cs, c->engine_done, 0));
   for (int i = 0; i < e.nframes; i++) {
-    const int slot = e.fr[i].slot;
+    const int slot = c->pend[i].slot;
     Stage& s = c->st[slot];
     CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
                       hipMemcpyDeviceToHost, c->cs));
@@ -276,7 +299,7 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   c->plane_elems = (size_t)c->wa * c->ha * 3 / 2;
   c->mbs = (size_t)c->wmb * c->hmb;
   c->nref = ring > 1 ? ring - 1 : 1;
-  c->sync_words = (size_t)SyncLayout::words((int)c->hmb);
+  c->sync_words = (size_t)SyncLayout::words((int)c->hmb, (int)(c->wmb + 3) / 4);
   int r = kSuccess;
 #define TRY(x)                         \
   do {                                 \
@@ -295,11 +318,28 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * kStages));
   TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * kStages));
   TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * kStages));
-  TRY(hipMalloc(&c->gran, c->mbs * kGranulesPerMB * sizeof(uint64_t) * kStages));
+  TRY(hipMalloc(&c->gran, c->mbs * kGranuleStride * sizeof(uint64_t) * kStages));
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * kStages));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t)));
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
+  {  // (frame, row) task order of the engine pools, for every batch size
+    const int hmb = (int)c->hmb, per = kMaxBatch * hmb;
+    std::vector<int32_t> ord((size_t)kMaxBatch * per, 0);
+    for (int nf = 1; nf <= kMaxBatch; nf++) {
+      int32_t* o = &ord[(size_t)(nf - 1) * per];
+      int n = 0;
+      for (int d = 0; d < hmb + kOrderSlope * nf; d++)
+        for (int f = 0; f < nf; f++) {
+          const int r = d - kOrderSlope * f;
+          if (r >= 0 && r < hmb) o[n++] = (f << 16) | r;
+        }
+    }
+    TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kStages * kMaxBatch, hipHostMallocDefault));
+    TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kStages * kMaxBatch));
+    TRY(hipMalloc(&c->order, ord.size() * sizeof(int32_t)));
+    TRY(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   for (auto& s : c->st) {
     TRY(hipHostMalloc(&s.table, c->mbs * sizeof(BlockDesc), hipHostMallocDefault));
     TRY(hipHostMalloc(&s.coef, c->plane_elems * 2, hipHostMallocDefault));
@@ -491,6 +531,18 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
   if (r) return r;
   if ((flags & 1) && !c->predeblock) CK(hipMalloc(&c->predeblock, c->plane_elems * 2));
   if ((flags & 2) && !c->stamps) CK(hipMalloc(&c->stamps, stamp_words(c) * sizeof(uint64_t)));
+  if ((flags & 4) && !c->trace_host) {
+    CK(hipHostMalloc(&c->trace_host, 4096 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->trace_host, 0xFF, 4096 * sizeof(int32_t));
+    CK(hipHostGetDevicePointer((void**)&c->trace_dev, c->trace_host, 0));
+  }
+  return kSuccess;
+}
+
+// Diagnostic: the live trace words (no synchronization; readable while the engine runs).
+int cairo_ctx_read_trace(cairo_ctx* c, int32_t* out, int n) {
+  if (!c || !c->trace_host || !out || n < 0 || n > 4096) return kInvalidArg;
+  memcpy(out, (const void*)c->trace_host, n * sizeof(int32_t));
   return kSuccess;
 }
 

@@ -26,17 +26,23 @@ __host__ __device__ inline PlaneSet ring_slot(int16_t* base, size_t slot_elems, 
 }
 
 // Granule hand-off of a reconstructed macroblock (MI355X_MICROARCH.md, R2 form):
-// 8-byte {high: tag = frame epoch, low: two int16 pixels}, each written by
-// ONE sc1 store; the reader polls the data itself.  Layout per macroblock:
-// 128 luma dwords (row r, pair d at r*8+d), then 32 U and 32 V (row r, pair d
-// at r*4+d).
-constexpr int kGranulesPerMB = 192;
+// 8-byte {high: tag = frame epoch, low: payload}, each written by ONE sc1
+// store; the reader polls the data itself.  Per macroblock: 128 luma dwords
+// (row r, pair d at r*8+d), 32 U and 32 V (row r, pair d at r*4+d), then one
+// info granule (copy << 8 | q_index) for the deblock.
+constexpr int kGranulesPerMB = 192;   // pixel granules
+constexpr int kGranuleStride = 193;   // + info granule
 
 // Phase boundaries recorded per macroblock by the row code when stamps != nullptr.
 constexpr int kStampPhases = 12;  // 10 real-time stamps + 2 shader-clock stamps
-// ...followed by kDbStamps per MB row: deblock phases 0..7, and 8 = the row
-// coder's "row coded" publish; then 2 words: engine entry (min) / exit (max).
-constexpr int kDbStamps = 9;
+// ...followed by kDbStamps per MB row: the deblock's publish time of each
+// column chunk; then 2 words: engine entry (min) / exit (max).
+constexpr int kDbStamps = 256;
+// Stamps of frame j of a batch start at j * stamp_frame_words; the 2 engine
+// words follow the kMaxBatch frames.
+__host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
+  return (size_t)wmb * hmb * kStampPhases + (size_t)hmb * kDbStamps;
+}
 
 // Frames per engine launch.
 constexpr int kMaxBatch = 16;
@@ -52,7 +58,9 @@ struct FrameDesc {
   int prev_slot;       // staging slot of the previous frame (output_cache chain)
 };
 
-// Per-frame view of the engine's state (built on the device from EngineArgs).
+// Per-frame view of the engine's state, built by the host for every frame of
+// a launch and read by the kernels from device memory (never copied into
+// private memory).
 struct FrameArgs {
   int wa, ha;          // frame size aligned to 16 (evx1enc.cpp:79-80)
   int w, h;            // nominal frame size (RGB input)
@@ -68,33 +76,44 @@ struct FrameArgs {
   BlockDesc* table;    // [wmb*hmb]
   BlockDesc* inter_desc;  // [(off-1)*mbs + mb]
   int32_t* inter_sad;     // [(off-1)*mbs + mb]
-  uint64_t* granules;  // [mbs * kGranulesPerMB]
+  uint64_t* granules;  // [mbs * kGranuleStride]
   int32_t* err;        // batch error word (a bounded wait timed out)
   int32_t* sticky;     // timeout flag that is never cleared (reported by the host)
-  int32_t* inter_done; // [hmb] inter-search tasks finished per MB row
-  int32_t* coded;      // [hmb] MB row coded (slot + table + coefficients written)
-  int32_t* deblocked;  // [hmb] MB row deblocked
+  int ng;              // inter-search groups (4 MBs) per row
+  int nref;            // inter-search tasks per group (references; 1 carrier task for intra frames)
+  int32_t* inter_done; // [hmb][ng] inter-search tasks finished
+  int32_t* deblocked;  // [hmb] final luma columns per MB row (monotone)
+  const int32_t* prev_deblocked;  // the previous frame's, if it is in this batch (else nullptr)
   uint64_t* stamps;    // diagnostic (nullptr = off)
+  const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)
 };
 
-// Words of the batch sync area (int32, zeroed per batch).
+// Build the view of frame j of a launch (host side; kernels.h layout rules).
+struct EngineArgs;
+FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j);
+
+// Words of the batch sync area (int32, zeroed per batch).  ng = inter-search
+// groups per MB row ((wmb + 3) / 4).
 struct SyncLayout {
   static constexpr int kErr = 0;
-  static constexpr int kTicketInter = 1;
   static constexpr int kTicketRows = 2;
-  static constexpr int kTicketDeblock = 3;
-  static constexpr int kFlags = 8;  // then per frame j: inter_done, coded, deblocked [hmb each]
-  __host__ __device__ static int inter_done(int hmb, int j) { return kFlags + 3 * hmb * j; }
-  __host__ __device__ static int coded(int hmb, int j) { return kFlags + 3 * hmb * j + hmb; }
-  __host__ __device__ static int deblocked(int hmb, int j) { return kFlags + 3 * hmb * j + 2 * hmb; }
-  __host__ __device__ static int words(int hmb) { return kFlags + 3 * hmb * kMaxBatch + 8; }
+  static constexpr int kTicketHelpers = 3;
+  static constexpr int kFlags = 8;
+  // per frame j: inter_done[hmb][ng] (tasks finished per group), then
+  // deblocked[hmb] (luma columns of the MB row that are final)
+  __host__ __device__ static int frame_words(int hmb, int ng) { return hmb * (ng + 1); }
+  __host__ __device__ static int inter_done(int hmb, int ng, int j) { return kFlags + frame_words(hmb, ng) * j; }
+  __host__ __device__ static int deblocked(int hmb, int ng, int j) {
+    return kFlags + frame_words(hmb, ng) * j + hmb * ng;
+  }
+  __host__ __device__ static int words(int hmb, int ng) { return kFlags + frame_words(hmb, ng) * kMaxBatch + 8; }
 };
 
 // One engine launch: up to kMaxBatch consecutive frames, pipelined.
 struct EngineArgs {
   int wa, ha, w, h, wmb, hmb, ring;
   int nframes;
-  FrameDesc fr[kMaxBatch];
+  const FrameArgs* fa;     // [nframes] per-frame views, device memory
   // per-slot buffers: base + slot * stride
   int16_t* src_base;    // plane sets, stride plane_elems
   int16_t* coef_base;   // plane sets, stride plane_elems
@@ -102,13 +121,22 @@ struct EngineArgs {
   BlockDesc* table_base;   // stride mbs
   BlockDesc* idesc_base;   // stride nref * mbs
   int32_t* isad_base;      // stride nref * mbs
-  uint64_t* gran_base;     // stride mbs * kGranulesPerMB
+  uint64_t* gran_base;     // stride mbs * kGranuleStride
   int16_t* ring_base;      // R reconstruction slots, stride plane_elems
   int32_t* sync;           // SyncLayout words
   int32_t* sticky;
   uint64_t* stamps;
-  int n_inter, n_rows, n_deblock;  // worker pools (workgroups), in blockIdx order
+  int n_helpers, n_rows;   // worker pools (workgroups); blockIdx order: helpers, rows
+  int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)
+  const int32_t* order;    // [nframes * hmb] task order of every pool: (frame << 16 | row),
+                           // sorted by (row + kOrderSlope * frame, frame)
 };
+
+// Frame-row task order of the engine pools.  A task of frame f, row r waits
+// at most on frame f-1, row r+3, so any slope > 3 keeps every wait pointing
+// to an earlier key (deadlock-free), while frames interleave in the pools
+// instead of queueing behind each other.
+constexpr int kOrderSlope = 6;
 
 // RGB -> YUV of every frame of the batch into its slot's source planes.
 hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);

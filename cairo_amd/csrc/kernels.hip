@@ -70,6 +70,23 @@ __device__ __forceinline__ int wave_max(int v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Diagnostic live trace (mapped host memory, system scope): word k of this workgroup.
+__device__ int32_t* g_trace_dummy;
+__device__ __forceinline__ void trace(int32_t* t, int k, int v) {
+  if (t && threadIdx.x == 0)
+    __hip_atomic_store(&t[blockIdx.x * 4 + k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Plane pl (0 Y, 1 U, 2 V) of a plane set.  The three pointers are read as
+// values and then selected: selecting between the fields' addresses would keep
+// the struct in scratch memory.
+__device__ __forceinline__ int16_t* pick(const PlaneSet& p, int pl) {
+  int16_t* const y = p.y;
+  int16_t* const u = p.u;
+  int16_t* const v = p.v;
+  return pl == 0 ? y : (pl == 1 ? u : v);
+}
+
 // A value every lane holds identically, moved to an SGPR so that the code
 // consuming it is scalar (no exec-mask divergence).
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -174,11 +191,11 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
 // ---------------------------------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_convert_batch(EngineArgs e) {
-  const FrameDesc& f = e.fr[blockIdx.z];
+  const FrameArgs& f = e.fa[blockIdx.z];
   const int qx = blockIdx.x * 256 + threadIdx.x;  // quad column
   const int qy = blockIdx.y;                      // quad row
   if (qx >= (e.w >> 1)) return;
-  const PlaneSet in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
+  const PlaneSet in = f.in;
   int su = 0, sv = 0;
 #pragma unroll
   for (int dy = 0; dy < 2; dy++) {
@@ -234,7 +251,7 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
     const int r = kk >> 3, c = (kk & 7) * 8;
     const int gy = coy + r, gx = cox + c;
     if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
-      const int16_t* src = pl ? p.v : p.u;
+      const int16_t* src = pick(p, 1 + pl);
       int16_t* dst = pl ? w.v : w.u;
       *(int4*)&dst[r * kWinCP + c] = *(const int4*)&src[(size_t)gy * cw + gx];
     }
@@ -519,7 +536,7 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(&a.inter_done[r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -687,133 +704,222 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
   return (cl && cr) ? 0 : ((cl != cr) ? 1 : 2);
 }
 
-// One deblock phase over a plane: n independent 8-sample lines.  Line i is
-// the 8 samples around an edge; `at(i)` gives its centre (the first q sample)
-// and `q(i, l, r)` the table-cache entries on both sides.  Vertical edges
-// (kRow: the line runs along a pixel row) load and store each line as two
-// 8-byte words; horizontal edges (column lines, stride `width`) one int16 per
-// lane per row, coalesced across lanes.  Every line of this thread's batch is
-// loaded before any is filtered, and lines of one phase never overlap (see
-// above), so whole lines are stored back.
-template <bool kRow, int kB, typename At, typename Q>
-__device__ __forceinline__ void db_phase(int16_t* img, int n, int width, bool luma, const int16_t* dq,
-                                         At at, Q q) {
-  for (int i0 = 0; i0 < n; i0 += 256 * kB) {
-    int v[kB][8], st[kB], qp[kB];
-    size_t off[kB];
-#pragma unroll
-    for (int b = 0; b < kB; b++) {
-      const int i = i0 + b * 256 + (int)threadIdx.x;
-      st[b] = 0;
-      if (i < n) {
-        off[b] = at(i);
-        int lq, rq;
-        q(i, lq, rq);
-        st[b] = edge_strength_q(dq[lq], dq[rq], qp[b]);
-        if (kRow) {
-          const short4 lo = *(const short4*)(img + off[b] - 4), hi = *(const short4*)(img + off[b]);
-          v[b][0] = lo.x, v[b][1] = lo.y, v[b][2] = lo.z, v[b][3] = lo.w;
-          v[b][4] = hi.x, v[b][5] = hi.y, v[b][6] = hi.z, v[b][7] = hi.w;
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++) v[b][k] = img[off[b] + (ptrdiff_t)(k - 4) * width];
-        }
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < kB; b++) {
-      if (!st[b]) continue;
-      int w[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) w[k] = v[b][k];
-      dfilter_reg(w, qp[b], st[b], luma);
-      if (kRow) {
-        if (w[1] != v[b][1] || w[2] != v[b][2] || w[3] != v[b][3] || w[4] != v[b][4] ||
-            w[5] != v[b][5] || w[6] != v[b][6]) {
-          *(short4*)(img + off[b] - 4) = make_short4(w[0], w[1], w[2], w[3]);
-          *(short4*)(img + off[b]) = make_short4(w[4], w[5], w[6], w[7]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 1; k < 7; k++)
-          if (w[k] != v[b][k]) img[off[b] + (ptrdiff_t)(k - 4) * width] = (int16_t)w[k];
-      }
-    }
-  }
+// Column-granular deblock of MB row r (whole workgroup), trailing the row
+// coder one macroblock (16 luma columns) at a time.  Inputs: row r's
+// pre-deblock pixels and block info from its granules; the 4 pixel rows above
+// (row r-1's final output, sc1) once row r-1's progress word passes the chunk.
+// All filtering happens in a circular LDS tile (luma rows 16r-4..16r+15 x 128
+// columns, chroma rows 8r-4..8r+7 x 64).  Per chunk [c0, c1):
+//   band A (luma band 2r, chroma band r): H edges of [c0, c1), then V edges
+//     of the units in [c0, c1);
+//   band B (luma band 2r+1): its H edge at column x reads band A rows that
+//     band A's V edges at units <= x+8 rewrite, so H runs up to c1-8 and its
+//     V edges (which read H's columns u-4..u+3) up to unit c1-16;
+// then every column no later edge touches (< c1-12) is written out with sc1
+// stores and published as the row's progress.  Row r needs row r-1 one
+// macroblock ahead, while the row coders run two apart: the deblock keeps
+// up instead of drifting.
+constexpr int kDbChunk = 16;
+constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
+constexpr int kDbCW = 64, kDbCP = 66;    // chroma
+
+struct DbLds {
+  int16_t y[20 * kDbLP];      // rows 16r-4 .. 16r+15
+  int16_t u[12 * kDbCP];      // rows 8r-4 .. 8r+7
+  int16_t v[12 * kDbCP];
+  int16_t info[2][8];         // (copy << 8 | q_index) of MB rows r-1 (0), r (1), column & 7
+};
+
+__device__ __forceinline__ int16_t* db_px(DbLds& D, int pl, int row, int col) {
+  if (pl == 0) return &D.y[row * kDbLP + (col & (kDbLW - 1))];
+  return &(pl == 1 ? D.u : D.v)[row * kDbCP + (col & (kDbCW - 1))];
 }
 
-// Horizontal edges at row j (column filters) / vertical edges of the band at
-// row j (row filters, units x >= 1) of one plane.  dq: table cache of MB rows
-// (j / mbsz) - 1 (entries 0..wib-1) and j / mbsz (entries wib..2*wib-1).
-__device__ __forceinline__ void db_h(int16_t* img, int width, int mbsz, int j, bool luma,
-                                     const int16_t* dq, bool interior) {
-  const int wib = width / mbsz;
-  db_phase<false, 4>(img, width, width, luma, dq,
-                     [=](int col) { return (size_t)j * width + col; },
-                     [=](int col, int& l, int& r) {
-                       l = (interior ? wib : 0) + col / mbsz;
-                       r = wib + col / mbsz;
-                     });
-}
-__device__ __forceinline__ void db_v(int16_t* img, int width, int mbsz, int j, bool luma,
-                                     const int16_t* dq) {
-  const int wib = width / mbsz;
-  db_phase<true, 4>(img, width - 8, width, luma, dq,
-                    [=](int i) { return (size_t)(j + (i & 7)) * width + ((i >> 3) + 1) * 8; },
-                    [=](int i, int& l, int& r) {
-                      const int x = (i >> 3) + 1;
-                      l = wib + (x * 8 - 1) / mbsz;
-                      r = wib + (x * 8) / mbsz;
-                    });
+// One 8-sample line through an edge, filtered in the tile.  Horizontal edge
+// (vertical line): samples at (row0 + k, col); vertical edge: (row0, col0 + k).
+__device__ __forceinline__ void db_line(DbLds& D, int pl, bool vert_line, int row0, int col0, int lq,
+                                        int rq) {
+  int qp;
+  const int st = edge_strength_q(lq, rq, qp);
+  if (!st) return;
+  int v[8], w[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    v[k] = w[k] = *db_px(D, pl, vert_line ? row0 + k : row0, vert_line ? col0 : col0 + k);
+  dfilter_reg(w, qp, st, pl == 0);
+#pragma unroll
+  for (int k = 1; k < 7; k++)
+    if (w[k] != v[k]) *db_px(D, pl, vert_line ? row0 + k : row0, vert_line ? col0 : col0 + k) = (int16_t)w[k];
 }
 
-// Deblock MB row r of frame a once row r is coded and row r-1 is filtered
-// (whole workgroup).  The row coders never wait on the deblock (no deadlock).
-// dq: LDS scratch of 2 * wmb int16.
-__device__ __forceinline__ void deblock_task(const FrameArgs& a, int r, int16_t* dq) {
+__device__ __forceinline__ const uint64_t* gran_mb(const FrameArgs& a, int mbx, int mby) {
+  return a.granules + (size_t)(mby * a.wmb + mbx) * kGranuleStride;
+}
+
+// Deblock progress of one MB row: next chunk, columns written, band B's next
+// H column and next V unit.
+struct DbState {
+  int k, w0, hb0, vb0;
+};
+
+// Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
+// Evaluated by thread 0 only.
+__device__ __forceinline__ bool deblock_chunk_ready(const FrameArgs& a, int r, const DbState& st) {
+  const int c1 = min((st.k + 1) * kDbChunk, a.wa);
+  if (r > 0 && __hip_atomic_load(&a.deblocked[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1)
+    return false;
+  const uint64_t g = gran_ld(gran_mb(a, st.k, r) + kGranulesPerMB);  // info granule, stored last
+  return (uint32_t)(g >> 32) == a.epoch;
+}
+
+// Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs).
+__device__ __forceinline__ void deblock_chunk(const FrameArgs& a, int r, DbLds& D, DbState& st) {
+  const int tid = threadIdx.x;
   const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
   const int cw = a.wa >> 1;
-  uint64_t* ds = a.stamps ? a.stamps + (size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps : nullptr;
-#define DB_STAMP(k) \
-  if (ds && threadIdx.x == 0) ds[k] = __builtin_amdgcn_s_memrealtime();
-  DB_STAMP(0);
-  if (threadIdx.x == 0) {
-    wait_at_least(&a.coded[r], 1, a.err, a.sticky);
-    if (r > 0) wait_at_least(&a.deblocked[r - 1], 1, a.err, a.sticky);
-  }
-  DB_STAMP(1);
-  acquire_after_wait();
-  DB_STAMP(2);
-  for (int i = threadIdx.x; i < 2 * a.wmb; i += 256) {
-    const int row = r - 1 + (i >= a.wmb), col = i >= a.wmb ? i - a.wmb : i;
-    int e = 0;
-    if (row >= 0) {
-      const BlockDesc& d = a.table[row * a.wmb + col];
-      e = ((d.block_type & kCopy) ? 0x100 : 0) | d.q_index;
+  const int y0 = 16 * r - 4, c0y = 8 * r - 4;  // tile origins (pixel rows)
+  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  int32_t* prog = a.deblocked;
+  int& w0 = st.w0;
+  int& hb0 = st.hb0;
+  int& vb0 = st.vb0;
+  {
+    const int k = st.k;
+    const int c0 = k * kDbChunk, c1 = min(c0 + kDbChunk, a.wa);
+    const bool last = k == nch - 1;
+    // ---- inputs of chunk k ----
+    if (r > 0 && tid == 0) {  // rows above final through column c1
+      if (__hip_atomic_load(&prog[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&prog[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1) {
+          if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
     }
-    dq[i] = (int16_t)e;
+    __syncthreads();
+    {  // pre-deblock pixels of MB c0/16 of row r (granules) + block info
+      const int m = c0 >> 4;
+      if (tid < kGranulesPerMB) {
+        const uint64_t* gp = gran_mb(a, m, r) + tid;
+        const uint32_t d = gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
+        int pl, row, col;
+        if (tid < 128) {
+          pl = 0, row = 4 + (tid >> 3), col = m * 16 + 2 * (tid & 7);
+        } else {
+          const int u = tid - 128;
+          pl = 1 + (u >> 5), row = 4 + ((u & 31) >> 2), col = m * 8 + 2 * (u & 3);
+        }
+        int16_t* p = db_px(D, pl, row, col);
+        p[0] = (int16_t)(d & 0xFFFF);
+        p[1] = (int16_t)(d >> 16);
+      } else if (tid < kGranulesPerMB + 2) {
+        const int row = r - 1 + (tid - kGranulesPerMB);
+        int e = 0;
+        if (row >= 0) {
+          const uint64_t* gp = gran_mb(a, m, row) + kGranulesPerMB;
+          e = (int)gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
+        }
+        D.info[tid - kGranulesPerMB][m & 7] = (int16_t)e;
+      } else if (r > 0) {  // 4 final rows above: luma 4 x 8 dwords, chroma 2 x 4 x 4 (sc1)
+        for (int i = tid - kGranulesPerMB - 2; i < 32 + 32; i += 256 - kGranulesPerMB - 2) {
+          int pl, row, col;
+          const int16_t* g;
+          if (i < 32) {
+            pl = 0, row = i >> 3, col = c0 + 2 * (i & 7);
+            g = cs.y + (size_t)(y0 + row) * a.wa + col;
+          } else {
+            const int j = i - 32, pj = j >> 4, jj = j & 15;
+            pl = 1 + pj, row = jj >> 2, col = (c0 >> 1) + 2 * (jj & 3);
+            g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
+          }
+          const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          int16_t* p = db_px(D, pl, row, col);
+          p[0] = (int16_t)(d & 0xFFFF);
+          p[1] = (int16_t)(d >> 16);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- band A: H edges of [c0, c1) (luma 16 + 2 x 8 chroma columns) ----
+    if (r > 0 && tid < 32) {
+      if (tid < 16) {
+        const int col = c0 + tid;
+        db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
+      } else {
+        const int pl = 1 + ((tid - 16) >> 3), col = (c0 >> 1) + (tid & 7);
+        db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
+      }
+    }
+    __syncthreads();
+    // ---- band A: V edges of units c0, c0+8 (luma) and c0/2 (chroma) ----
+    if (tid < 32) {
+      if (tid < 16) {
+        const int x = c0 + 8 * (tid >> 3), row = 4 + (tid & 7);
+        if (x > 0 && x < c1)
+          db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
+      } else {
+        const int pl = 1 + ((tid - 16) >> 3), x = c0 >> 1, row = 4 + (tid & 7);
+        if (x > 0)
+          db_line(D, pl, false, row, x - 4, D.info[1][((x - 1) >> 3) & 7], D.info[1][(x >> 3) & 7]);
+      }
+    }
+    __syncthreads();
+    // ---- band B: H edges of [hb0, hb1), then V edges of units [vb0, vb1) ----
+    const int hb1 = last ? a.wa : c1 - 8, vb1 = last ? a.wa : c1 - 8;
+    for (int col = hb0 + tid; col < hb1; col += 256)
+      db_line(D, 0, true, 8, col, D.info[1][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
+    __syncthreads();
+    for (int i = tid; i < 8 * ((vb1 - vb0 + 7) >> 3); i += 256) {
+      const int x = vb0 + 8 * (i >> 3), row = 12 + (i & 7);
+      if (x < vb1) db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
+    }
+    __syncthreads();
+    hb0 = max(hb0, hb1);
+    vb0 = max(vb0, vb1);
+    const int w1 = last ? a.wa : max(w0, c1 - 12);
+    // ---- write out columns [w0, w1): luma rows 16r-3..16r+15, chroma 8r-3..8r+7 ----
+    if (w1 > w0) {
+      const int rl0 = r > 0 ? 1 : 4, rc0 = r > 0 ? 1 : 4;  // first tile row written
+      const int nl = (w1 - w0) >> 1, nc = (w1 - w0) >> 2;
+      const int nrl = 20 - rl0, nrc = 12 - rc0;
+      for (int i = tid; i < nrl * nl + 2 * nrc * nc; i += 256) {
+        int pl, row, col;
+        int16_t* g;
+        if (i < nrl * nl) {
+          pl = 0, row = rl0 + i / nl, col = w0 + 2 * (i % nl);
+          g = cs.y + (size_t)(y0 + row) * a.wa + col;
+        } else {
+          const int j = i - nrl * nl, pj = j / (nrc * nc), jj = j % (nrc * nc);
+          pl = 1 + pj, row = rc0 + jj / nc, col = (w0 >> 1) + 2 * (jj % nc);
+          g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
+        }
+        const int16_t* p = db_px(D, pl, row, col);
+        const uint32_t d = (uint32_t)(uint16_t)p[0] | ((uint32_t)(uint16_t)p[1] << 16);
+        __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)g, d, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(&prog[r], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.stamps && tid == 0 && k < kDbStamps)
+        a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps + k] = __builtin_amdgcn_s_memrealtime();
+      w0 = w1;
+    }
   }
-  __syncthreads();
-  DB_STAMP(3);
-  if (r > 0) {  // band 2r (luma) / r (chroma): top edges, then vertical edges
-    db_h(cs.y, a.wa, 16, 16 * r, true, dq, false);
-    db_h(cs.u, cw, 8, 8 * r, false, dq, false);
-    db_h(cs.v, cw, 8, 8 * r, false, dq, false);
-  }
-  __syncthreads();
-  DB_STAMP(4);
-  db_v(cs.y, a.wa, 16, 16 * r, true, dq);
-  db_v(cs.u, cw, 8, 8 * r, false, dq);
-  db_v(cs.v, cw, 8, 8 * r, false, dq);
-  __syncthreads();
-  DB_STAMP(5);
-  db_h(cs.y, a.wa, 16, 16 * r + 8, true, dq, true);  // band 2r+1: MB-interior edge
-  __syncthreads();
-  DB_STAMP(6);
-  db_v(cs.y, a.wa, 16, 16 * r + 8, true, dq);
-  publish(&a.deblocked[r], 1);
-  DB_STAMP(7);
-#undef DB_STAMP
+  st.k++;
+}
+
+__device__ __forceinline__ void deblock_task(const FrameArgs& a, int r, DbLds& D) {
+  DbState st{0, 0, 0, 8};
+  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  while (st.k < nch) deblock_chunk(a, r, D, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -854,7 +960,7 @@ struct alignas(16) RowLds {
 __device__ __forceinline__ const int16_t* win_src(const PlaneSet& p, int wa, int mbx, int mby, int k) {
   if (k < 128) return p.y + (size_t)(mby * 16 + (k >> 3)) * wa + mbx * 16 + 2 * (k & 7);
   const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
-  return (pl ? p.v : p.u) + (size_t)(mby * 8 + r) * (wa >> 1) + mbx * 8 + 2 * d;
+  return pick(p, 1 + pl) + (size_t)(mby * 8 + r) * (wa >> 1) + mbx * 8 + 2 * d;
 }
 __device__ __forceinline__ uint32_t* win_dst(RowWindow& w, int oy, int mbx, int mby, int k) {
   if (k < 128) {
@@ -948,7 +1054,7 @@ __device__ __forceinline__ int win_px(const RowWindow& w, int oy, int pl, int ex
 }
 
 __device__ __forceinline__ const int16_t* plane_of(const PlaneSet& p, int pl) {
-  return pl == 0 ? p.y : (pl == 1 ? p.u : p.v);
+  return pick(p, pl);
 }
 
 // Prediction sample of element e (block-major) of the block at (mx, my) of
@@ -984,12 +1090,27 @@ __device__ __forceinline__ BlockDesc uni_desc(const BlockDesc& d) {
 }
 
 __device__ __forceinline__ uint64_t* gran_at(const FrameArgs& a, int mbx, int mby, int k) {
-  return a.granules + (size_t)(mby * a.wmb + mbx) * kGranulesPerMB + k;
+  return a.granules + (size_t)(mby * a.wmb + mbx) * kGranuleStride + k;
+}
+
+// Store lane pairs (lane, lane^1) of an 8x8 block's int16 values as dwords
+// with write-through (sc1) stores: the next frame reads them back (output_cache
+// carry of copy macroblocks) on another CU.  e = element (block-major).
+__device__ __forceinline__ void coef_store_pair(const FrameArgs& a, int e, int px, int py, int value) {
+  const int nb = __builtin_amdgcn_mov_dpp(value, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+  if (!(threadIdx.x & 1)) {
+    int pl, ex, ey;
+    elem_coords(e, px, py, pl, ex, ey);
+    int16_t* cp = pick(a.coef, pl);
+    __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(cp + (size_t)ey * (pl ? a.wa >> 1 : a.wa) + ex),
+                       ((uint32_t)value & 0xFFFFu) | ((uint32_t)nb << 16), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Code MB row `by` of frame a (intra search, classify, transform, VAQ,
 // quantize, reconstruct), left to right; whole workgroup.
-__device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) {
+__device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, int32_t* tr) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
@@ -1003,8 +1124,13 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) 
     const int py = by * kMB, oy = py - 48;
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
+      trace(tr, 1, bx);
       stamp(a, mb, 0);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
+      if ((bx & 3) == 0) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
+        if (tid == 0) wait_at_least(&a.inter_done[by * a.ng + (bx >> 2)], a.nref, err, a.sticky);
+        acquire_after_wait();
+      }
 
       // ---- window.  Reconstruction of the rows above arrives as granules
       //      (this frame's data, polled by tag); the stale row below is the
@@ -1198,10 +1324,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) 
         _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
           const int b = wave + 4 * bi, e = b * 64 + lane;
           const int16_t qv = quant_elem(e, cf[bi], qp, intra_path);
-          int pl, ex, ey;
-          elem_coords(e, px, py, pl, ex, ey);
-          int16_t* cp = pl == 0 ? a.coef.y : (pl == 1 ? a.coef.u : a.coef.v);
-          cp[(size_t)ey * (pl ? cw : a.wa) + ex] = qv;
+          coef_store_pair(a, e, px, py, qv);
           const int t = idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
                                   dequant_elem(e, qv, qp, intra_path));
           pv[bi] = (int16_t)(has_pred ? t + pv[bi] : t);  // reconstruction (unclamped)
@@ -1214,18 +1337,16 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) 
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
           const size_t o = (size_t)ey * (pl ? cw : a.wa) + ex;
-          (pl == 0 ? a.coef.y : (pl == 1 ? a.coef.u : a.coef.v))[o] =
-              (pl == 0 ? a.coef_prev.y : (pl == 1 ? a.coef_prev.u : a.coef_prev.v))[o];
+          coef_store_pair(a, e, px, py, pick(a.coef_prev, pl)[o]);
         }
       }
       stamp(a, mb, 7);
-      // reconstruction -> current slot (global) and the window
+      // reconstruction -> the window (the slot is written by the deblock,
+      // from the granules)
       _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
         const int b = wave + 4 * bi, e = b * 64 + lane;
         int pl, ex, ey;
         elem_coords(e, px, py, pl, ex, ey);
-        int16_t* p = pl == 0 ? cs.y : (pl == 1 ? cs.u : cs.v);
-        p[(size_t)ey * (pl ? cw : a.wa) + ex] = (int16_t)pv[bi];
         if (pl == 0)
           L.win.y[(ey - oy) * kCwLP + (ex & 127)] = (int16_t)pv[bi];
         else
@@ -1242,7 +1363,10 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) 
       }
       if (tid == 0) a.table[mb] = d;
       stamp(a, mb, 8);
-      // publish: pixel pairs (lane, lane^1) of each 8x8 block as granules
+      // publish: pixel pairs (lane, lane^1) of each 8x8 block as granules.
+      // Drain first: whoever observes these granules (and everything causally
+      // after) must also see this MB's write-through coefficient stores.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
         const int b = wave + 4 * bi;
         const int nb = __builtin_amdgcn_mov_dpp(pv[bi], 0xB1, 0xF, 0xF, false);  // lane ^ 1
@@ -1253,118 +1377,168 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L) 
                   ((uint64_t)tag << 32) | ((uint32_t)pv[bi] & 0xFFFFu) | ((uint32_t)nb << 16));
         }
       }
+      if (tid == 0)  // block info for the deblock (its edge strengths)
+        gran_st(gran_at(a, bx, by, kGranulesPerMB),
+                ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index);
       stamp(a, mb, 9);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
-    publish(&a.coded[by], 1);  // row by coded: the deblock and later frames may use it
-    if (a.stamps && tid == 0)
-      a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)by * kDbStamps + 8] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
-__device__ __forceinline__ FrameArgs frame_view(const EngineArgs& e, int j) {
-  const FrameDesc& f = e.fr[j];
-  FrameArgs a;
-  a.wa = e.wa, a.ha = e.ha, a.w = e.w, a.h = e.h, a.wmb = e.wmb, a.hmb = e.hmb, a.ring = e.ring;
-  a.index = f.index;
-  a.inter = f.inter && e.ring > 1;
-  a.quality = f.quality;
-  a.epoch = f.epoch;
-  a.in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
-  a.coef = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.slot);
-  a.coef_prev = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.prev_slot);
-  a.ring_base = e.ring_base;
-  a.slot_elems = e.plane_elems;
-  const size_t mbs = (size_t)e.wmb * e.hmb, nref = e.ring > 1 ? e.ring - 1 : 1;
-  a.table = e.table_base + (size_t)f.slot * mbs;
-  a.inter_desc = e.idesc_base + (size_t)f.slot * nref * mbs;
-  a.inter_sad = e.isad_base + (size_t)f.slot * nref * mbs;
-  a.granules = e.gran_base + (size_t)f.slot * mbs * kGranulesPerMB;
-  a.err = e.sync + SyncLayout::kErr;
-  a.sticky = e.sticky;
-  a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, j);
-  a.coded = e.sync + SyncLayout::coded(e.hmb, j);
-  a.deblocked = e.sync + SyncLayout::deblocked(e.hmb, j);
-  a.stamps = e.stamps;
-  return a;
-}
+
+#ifndef CAIRO_HELPER_INTERLEAVE
+#define CAIRO_HELPER_INTERLEAVE 1
+#endif
+constexpr bool kHelperInterleave = CAIRO_HELPER_INTERLEAVE;
+
+struct HelperLds {
+  InterLds inter;
+  DbLds db;
+};
 
 struct EngineLds {
   union {
     RowLds row;
-    InterLds inter;
+    HelperLds helper;
   } u;
   int slot;
+  int flag;  // helper decisions broadcast from thread 0 (kept out of the union)
 };
+
+// Row helper (j, r): the inter search of MB row r, group by group as the
+// previous frame becomes final over each group's search window (the row
+// coder waits for exactly these), and the deblock of row r, chunk by chunk as
+// the coder's granules arrive (advanced whenever the inter search is waiting
+// or done).  Never blocks on its own row coder while an inter group is due.
+// Thread 0's value v, broadcast to the workgroup (two barriers).
+__device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
+  if (threadIdx.x == 0) *slot = v;
+  __syncthreads();
+  const int r = *slot;
+  __syncthreads();
+  return r;
+}
+
+// Helper decision for group g (thread 0): 1 = the inter search may run,
+// 2 = a deblock chunk is ready meanwhile, 0 = nothing yet.
+__device__ __forceinline__ int helper_decision(const FrameArgs& a, int r, int need, const DbState& st, int nch) {
+  const int rr = min(r + 3, a.hmb - 1);
+  if (!a.prev_deblocked ||
+      __hip_atomic_load(a.prev_deblocked + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
+    return 1;
+  if (kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st)) return 2;
+  return 0;
+}
+
+// Row helper (j, r): the inter search of MB row r, group by group as the
+// previous frame becomes final over each group's search window (the row
+// coder waits for exactly these), and the deblock of row r, chunk by chunk as
+// the coder's granules arrive (advanced whenever the inter search is waiting
+// or done).  Never blocks on its own row coder while an inter group is due.
+__device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds& L, int* flag, int32_t* tr) {
+  const int tid = threadIdx.x;
+  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  volatile int* vflag = flag;
+  DbState st{0, 0, 0, 8};
+  for (int g = 0; g < a.ng; g++) {
+    trace(tr, 1, g);
+    const int need = min(64 * g + 96, a.wa);
+    uint64_t t0 = 0;
+    for (;;) {  // until group g may run; deblock meanwhile
+      int d = 0;
+      if (tid == 0) {
+        d = helper_decision(a, r, need, st, nch);
+        if (d == 0) {  // nothing to do: back off, bounded like every wait
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (!t0) t0 = now;
+          __builtin_amdgcn_s_sleep(1);
+          if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            d = 1;
+          } else if (now - t0 > 200000000ull) {
+            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            d = 1;
+          }
+        }
+      }
+      d = wg_broadcast(vflag, d);
+      trace(tr, 3, 20 + d);
+      if (d == 1) break;
+      if (d == 2) deblock_chunk(a, r, L.db, st);
+    }
+    if (tid == 0) {  // the readiness check used a relaxed load: acquire what it observed
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    trace(tr, 3, 50);
+    if (a.inter) {
+      for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter);
+    } else if (tid == 0) {  // intra frame: carry the dependency only
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (;;) {  // catch the deblock up with what has arrived
+      int d = 0;
+      if (tid == 0) d = kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
+      if (!wg_broadcast(vflag, d)) break;
+      deblock_chunk(a, r, L.db, st);
+    }
+  }
+  trace(tr, 1, 1000);
+  while (st.k < nch) {
+    trace(tr, 2, st.k);
+    deblock_chunk(a, r, L.db, st);
+  }
+  trace(tr, 2, 100000);
+}
 
 // ---------------------------------------------------------------------------
 // The engine: one persistent launch encodes a batch of consecutive frames,
-// pipelined across frames.  Three worker pools (blockIdx ranges) dequeue
-// their tasks in (frame, row) order:
-//   inter    (j, r, g, off): inter search of MBs 4g..4g+3 of row r against
-//            reference offset off; needs the batch's references deblocked
-//            through MB row r+3 (the search reaches 47 rows below the row top,
-//            and the next row's deblock rewrites 3 of them);
-//   rows     (j, r): code MB row r; needs the row's inter records, the frames
-//            still reading this slot's previous content (j-1..j-R+1) coded
-//            through row r+2, and the stale rows below final (frame j-R
-//            deblocked through row r+2); rows above arrive as granules;
-//   deblock  (j, r): needs row r coded and row r-1 deblocked.
-// Every wait targets an earlier frame or an earlier stage/row of the same
-// frame, and each pool dequeues in order, so the oldest unfinished task is
-// always running: no deadlock with every workgroup resident.
+// pipelined across frames.  Two worker pools (blockIdx ranges: helpers, then
+// row coders) dequeue (frame, row) tasks in e.order (by row + slope * frame):
+//   helper (j, r): inter search of row r, group g (MBs 4g..4g+3) once the
+//           previous frame is final on MB rows r-2..r+2 over the group's
+//           search window [64g-32, 64g+96) (this also covers every older
+//           frame, transitively); and the deblock of row r behind its coder;
+//   rows   (j, r): code MB row r; before MBs 4g..4g+3 it waits for group g's
+//           inter records (and thereby every cross-frame dependency: the
+//           frames still reading this slot's old content are done with it
+//           there, the stale rows below are final); rows above arrive as
+//           granules.
+// Every wait targets an earlier frame, or an earlier row, or the same row's
+// other worker, which never waits back (a helper only polls its coder's
+// granules, without blocking, while an inter group is due).  Each pool
+// dequeues in order, so the oldest unfinished task always progresses: no
+// deadlock with every workgroup resident.
 // ---------------------------------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_engine(EngineArgs e) {
   __shared__ EngineLds L;
   const int b = blockIdx.x, hmb = e.hmb;
-  const int nref = e.ring > 1 ? e.ring - 1 : 0;
-  int32_t* err = e.sync + SyncLayout::kErr;
-  uint64_t* ks = e.stamps ? e.stamps + (size_t)e.wmb * hmb * kStampPhases + (size_t)hmb * kDbStamps : nullptr;
+  uint64_t* ks = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, hmb) : nullptr;
   if (ks && threadIdx.x == 0)
     __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int ng = (e.wmb + 3) >> 2;
-  if (b < e.n_inter) {
-    const int per_row = ng * nref, per_frame = hmb * per_row;
-    const int total = e.nframes * per_frame;
+  const int total = e.nframes * hmb;
+  if (b < e.n_helpers) {
     for (;;) {
-      const int t = dequeue(e.sync + SyncLayout::kTicketInter, &L.slot);
+      const int t = dequeue(e.sync + SyncLayout::kTicketHelpers, &L.slot);
+      trace(e.trace, 0, 1000000 + t);
       if (t >= total) break;
-      const int j = t / per_frame, rem = t - j * per_frame, r = rem / per_row;
-      const int rem2 = rem - r * per_row, g = rem2 / nref, off = rem2 - g * nref + 1;
-      const FrameArgs a = frame_view(e, j);
-      if (!a.inter) continue;
-      if (threadIdx.x == 0)
-        for (int o = 1; o <= nref && j - o >= 0; o++)
-          wait_at_least(e.sync + SyncLayout::deblocked(hmb, j - o) + min(r + 3, hmb - 1), 1, err, e.sticky);
-      acquire_after_wait();
-      inter_task(a, r, g, off, L.u.inter);
-    }
-  } else if (b < e.n_inter + e.n_rows) {
-    const int total = e.nframes * hmb;
-    for (;;) {
-      const int t = dequeue(e.sync + SyncLayout::kTicketRows, &L.slot);
-      if (t >= total) break;
-      const int j = t / hmb, r = t - j * hmb;
-      const FrameArgs a = frame_view(e, j);
-      if (threadIdx.x == 0) {
-        if (a.inter) wait_at_least(&a.inter_done[r], ng * nref, err, e.sticky);
-        for (int o = 1; o < e.ring && j - o >= 0; o++)
-          wait_at_least(e.sync + SyncLayout::coded(hmb, j - o) + min(r + 2, hmb - 1), 1, err, e.sticky);
-        if (j - e.ring >= 0)
-          wait_at_least(e.sync + SyncLayout::deblocked(hmb, j - e.ring) + min(r + 2, hmb - 1), 1, err,
-                        e.sticky);
-      }
-      acquire_after_wait();
-      code_row(a, r, L.u.row);
+      const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
+      row_helper(e.fa[j], r, L.u.helper, &L.flag, e.trace);
+      trace(e.trace, 0, 2000000 + t);
     }
   } else {
-    const int total = e.nframes * hmb;
     for (;;) {
-      const int t = dequeue(e.sync + SyncLayout::kTicketDeblock, &L.slot);
+      const int t = dequeue(e.sync + SyncLayout::kTicketRows, &L.slot);
+      trace(e.trace, 0, 3000000 + t);
       if (t >= total) break;
-      const int j = t / hmb, r = t - j * hmb;
-      deblock_task(frame_view(e, j), r, L.u.row.win.y);
+      const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
+      code_row(e.fa[j], r, L.u.row, e.trace);
+      trace(e.trace, 0, 4000000 + t);
     }
   }
   if (ks && threadIdx.x == 0)
@@ -1372,10 +1546,10 @@ __global__ __launch_bounds__(256) void k_engine(EngineArgs e) {
 }
 
 __global__ __launch_bounds__(192) void k_unpack_granules(EngineArgs e, int j, PlaneSet dst) {
-  const FrameArgs a = frame_view(e, j);
+  const FrameArgs& a = e.fa[j];
   const int mb = blockIdx.x, k = threadIdx.x;
   const int mbx = mb % a.wmb, mby = mb / a.wmb;
-  const uint32_t v = (uint32_t)a.granules[(size_t)mb * kGranulesPerMB + k];
+  const uint32_t v = (uint32_t)a.granules[(size_t)mb * kGranuleStride + k];
   int16_t* p;
   if (k < 128) {
     p = dst.y + (size_t)(mby * 16 + (k >> 3)) * a.wa + mbx * 16 + 2 * (k & 7);
@@ -1392,8 +1566,37 @@ hipError_t launch_unpack_granules(const EngineArgs& e, int j, PlaneSet dst, hipS
   return hipGetLastError();
 }
 
+FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
+  FrameArgs a{};
+  a.wa = e.wa, a.ha = e.ha, a.w = e.w, a.h = e.h, a.wmb = e.wmb, a.hmb = e.hmb, a.ring = e.ring;
+  a.index = f.index;
+  a.inter = f.inter && e.ring > 1;
+  a.quality = f.quality;
+  a.epoch = f.epoch;
+  a.in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
+  a.coef = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.slot);
+  a.coef_prev = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.prev_slot);
+  a.ring_base = e.ring_base;
+  a.slot_elems = e.plane_elems;
+  const size_t mbs = (size_t)e.wmb * e.hmb, nref = e.ring > 1 ? e.ring - 1 : 1;
+  a.table = e.table_base + (size_t)f.slot * mbs;
+  a.inter_desc = e.idesc_base + (size_t)f.slot * nref * mbs;
+  a.inter_sad = e.isad_base + (size_t)f.slot * nref * mbs;
+  a.granules = e.gran_base + (size_t)f.slot * mbs * kGranuleStride;
+  a.err = e.sync + SyncLayout::kErr;
+  a.sticky = e.sticky;
+  a.ng = (e.wmb + 3) >> 2;
+  a.nref = a.inter ? e.ring - 1 : 1;
+  a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, a.ng, j);
+  a.deblocked = e.sync + SyncLayout::deblocked(e.hmb, a.ng, j);
+  a.prev_deblocked = j > 0 ? e.sync + SyncLayout::deblocked(e.hmb, a.ng, j - 1) : nullptr;
+  a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
+  a.rgb = f.rgb;
+  return a;
+}
+
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s) {
-  hipLaunchKernelGGL(k_engine, dim3(e.n_inter + e.n_rows + e.n_deblock), dim3(256), 0, s, e);
+  hipLaunchKernelGGL(k_engine, dim3(e.n_helpers + e.n_rows), dim3(256), 0, s, e);
   return hipGetLastError();
 }
 

@@ -86,6 +86,9 @@ CAIRO_API int cairo_ctx_read_table(cairo_ctx *ctx, uint8_t *table);
  * per MB, 100 MHz clock; cairo_ctx_read_stamps). */
 CAIRO_API int cairo_ctx_set_debug(cairo_ctx *ctx, int flags);
 CAIRO_API int cairo_ctx_read_stamps(cairo_ctx *ctx, uint64_t *out);
+/* Debug: flags & 4 keeps a live per-workgroup state trace of the engine in
+ * mapped host memory; read it (n int32 words) without synchronizing. */
+CAIRO_API int cairo_ctx_read_trace(cairo_ctx *ctx, int32_t *out, int n);
 CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, int16_t *v);
 
 /* Per-kernel timing (HIP events on the kernels' stream), opt-in. */

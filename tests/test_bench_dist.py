@@ -2,7 +2,7 @@
 timing and the whole-job aggregate that rank 0 reports.  The GPU ranks run the
 same functions over RCCL (bench.py main)."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch.distributed as dist
@@ -11,17 +11,9 @@ import torch.multiprocessing as mp
 import bench
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store, out):
+    # file rendezvous: no TCP port to race for
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     elapsed = 1.0 + rank  # rank 1 is the slow one
     m = bench.max_over_ranks(elapsed, dist, "cpu")
     out[rank] = (m, bench.aggregate_mpix(1280, 720, 10, world, m))
@@ -31,10 +23,9 @@ def _worker(rank, world, port, out):
 
 def test_max_over_ranks_and_aggregate_gloo():
     world = 2
-    port = _free_port()
-    with mp.Manager() as mgr:
+    with tempfile.TemporaryDirectory() as tmp, mp.Manager() as mgr:
         out = mgr.dict()
-        mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "store"), out), nprocs=world, join=True)
         res = dict(out)
     for r in range(world):
         m, v = res[r]

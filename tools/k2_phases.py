@@ -1,9 +1,11 @@
-"""Per-phase timing of the macroblock wavefront kernel (k_mb_rows).
+"""Per-phase timing of the row coder inside the engine (diagnostic stamps).
 
-Runs a few frames with the diagnostic stamps on (cairo_ctx_set_debug(ctx, 2))
-and prints the mean duration of each phase of a macroblock, plus the
+Runs one warm-up batch and one measured batch of `--batch` frames with the
+stamps on (cairo_ctx_set_debug(ctx, 2)) and prints, for the measured batch:
+each frame's coding span inside the launch, the start lag between
+consecutive frames, the mean duration of each phase of a macroblock, and the
 producer-publish -> consumer-resume hand-off latency across rows.
-usage: python tools/k2_phases.py [--config 720p] [--frames 4]
+usage: python tools/k2_phases.py [--config 720p] [--batch 8]
 """
 import argparse
 import os
@@ -19,43 +21,97 @@ PHASES = ["wait", "window", "int_search", "subpel", "classify", "pred", "code", 
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="720p")
-ap.add_argument("--frames", type=int, default=4)
+ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--rows", type=int, default=0, help="row-coder workgroups (0 = default)")
 a = ap.parse_args()
 w, h, ring, q = CFG[a.config]
 ctx = cairo_amd.Context(w, h, ring)
 ctx.set_debug(2)
-for t in range(a.frames):
-    ctx.encode_frame(cairo_amd.make_band4(w, h, t), t, t > 0, q)
-    ctx.sync()
-st, dbs, kio = ctx.read_stamps()  # 10 ns ticks
+ctx.set_batch(a.batch)
+if a.rows:
+    ctx.set_workgroups(a.rows)
+B = a.batch
+for first in (0, B):  # warm-up batch, measured batch
+    frames = [cairo_amd.make_band4(w, h, t) for t in range(first, first + B)]
+    tks = [ctx.submit(f, first + i, first + i > 0, q) for i, f in enumerate(frames)]
+    for t in tks:
+        ctx.wait(t, copy=False)
+        ctx.release(t)
+st, dbs, kio, ist = ctx.read_stamps()  # 10 ns ticks
+dbs = dbs[:B].astype(np.int64)
+ist = ist[:B].astype(np.int64)
+st = st[:B].astype(np.int64)
 kio = kio.astype(np.int64)
-st, dbs = st.astype(np.int64), dbs.astype(np.int64)
-d = np.diff(st[..., :10], axis=2) / 100.0  # us
-print(f"{a.config} frame {a.frames - 1}: per-MB phase means (us) over {st.shape[0] * st.shape[1]} MBs")
+hb, wb = st.shape[1:3]
+steps = wb + 3 * (hb - 1)
+t0 = kio[0]
+print(f"{a.config} batch {B}: engine entry -> exit {(kio[1] - kio[0]) / 100.0:.1f} us "
+      f"({(kio[1] - kio[0]) / 100.0 / B:.1f} us per frame)")
+starts = []
+for j in range(B):
+    s0, s1 = st[j, ..., 0].min(), st[j, ..., 9].max()
+    starts.append(s0)
+    print(f"  frame {j}: coding {(s0 - t0) / 100.0:8.1f} .. {(s1 - t0) / 100.0:8.1f} us  "
+          f"span {(s1 - s0) / 100.0:7.1f} us = {(s1 - s0) / 100.0 / steps:.2f} us/step")
+if B > 1:
+    lag = np.diff(np.array(starts)) / 100.0
+    print(f"  start lag between frames: mean {lag.mean():.1f} us")
+d = np.diff(st[..., :10], axis=-1) / 100.0  # (B, hmb, wmb, 9) us
+print("per-MB phase means over the batch (us):")
 for k, name in enumerate(PHASES):
-    print(f"  {name:11s} mean {d[..., k].mean():8.3f}  p50 {np.median(d[..., k]):8.3f}  max {d[..., k].max():8.3f}")
+    print(f"  {name:11s} mean {d[..., k].mean():8.3f}  p50 {np.median(d[..., k]):8.3f}")
 tot = (st[..., 9] - st[..., 0]) / 100.0
 print(f"  total/MB    mean {tot.mean():8.3f}")
-# hand-off: MB (bx, by) resumes (stamp 1) after (bx+2, by-1) published (stamp 9)
-hb, wb = st.shape[:2]
 lat = []
-for by in range(1, hb):
-    for bx in range(wb):
-        src = min(bx + 2, wb - 1)
-        lat.append((st[by, bx, 1] - st[by - 1, src, 9]) / 100.0)
+for j in range(B):
+    for by in range(1, hb):
+        for bx in range(wb):
+            src = min(bx + 2, wb - 1)
+            lat.append((st[j, by, bx, 1] - st[j, by - 1, src, 9]) / 100.0)
 lat = np.array(lat)
 print(f"  hand-off (publish -> resume) mean {lat.mean():.3f} p50 {np.median(lat):.3f} us")
 clk = (st[..., 11] - st[..., 10]) / np.maximum(st[..., 9] - st[..., 0], 1) * 100.0  # MHz
-print(f"  effective shader clock: mean {clk.mean():.0f} MHz, p10 {np.percentile(clk, 10):.0f}, p90 {np.percentile(clk, 90):.0f}")
-span = (st[..., 9].max() - st[..., 0].min()) / 100.0
-print(f"  kernel span {span:.1f} us, steps {wb + 3 * (hb - 1)}, per step {span / (wb + 3 * (hb - 1)):.3f} us")
-# deblock workers: per row, phases relative to the row-coded publish (stamp 8)
-DBP = ["wait", "acquire", "table", "H band0", "V band0", "H band1", "V band1+pub"]
-dd = np.diff(dbs[:, :8], axis=1) / 100.0
-print("deblock per row (us): " + ", ".join(f"{n} {dd[:, k].mean():.2f}" for k, n in enumerate(DBP)))
-lag = (dbs[:, 7] - dbs[:, 8]) / 100.0
-print(f"  row coded -> row deblocked: mean {lag.mean():.2f} us, last row {lag[-1]:.2f} us")
-print(f"  last MB end -> last row deblocked: {(dbs[:, 7].max() - st[..., 9].max()) / 100.0:.2f} us")
-print(f"  kernel entry -> first MB: {(st[..., 0].min() - kio[0]) / 100.0:.2f} us; "
-      f"last row deblocked -> kernel exit: {(kio[1] - dbs[:, 7].max()) / 100.0:.2f} us; "
-      f"entry -> exit {(kio[1] - kio[0]) / 100.0:.1f} us")
+print(f"  effective shader clock: mean {clk.mean():.0f} MHz")
+# inter tasks: dequeue -> ready (dependency met) -> done
+ok = ist[..., 2] > 0
+if ok.any():
+    wait = (ist[..., 1] - ist[..., 0])[ok] / 100.0
+    run = (ist[..., 2] - ist[..., 1])[ok] / 100.0
+    print(f"inter tasks: {ok.sum()}  wait mean {wait.mean():.1f} us  run mean {run.mean():.1f} us p50 {np.median(run):.1f} "
+          f"max {run.max():.1f}")
+    for j in range(B):
+        okj = ist[j, ..., 2] > 0
+        if okj.any():
+            print(f"  frame {j}: inter tasks {(ist[j, ..., 0][okj].min() - t0) / 100.0:8.1f} .. "
+                  f"{(ist[j, ..., 2][okj].max() - t0) / 100.0:8.1f} us")
+# frame-to-frame lag of MB completion (stamp 9) at sample positions
+if B > 2:
+    print("lag of frame j+1 behind frame j at MB (x, r), us [j=0->1, 1->2, 2->3]:")
+    for r in (0, 5, 10, 20, 30, 40, hb - 1):
+        row = []
+        for x in (0, wb // 2, wb - 1):
+            lags = [(st[j + 1, r, x, 9] - st[j, r, x, 9]) / 100.0 for j in range(3)]
+            row.append(f"x={x:3d}: " + "/".join(f"{v:6.0f}" for v in lags))
+        print(f"  r={r:3d}  " + "   ".join(row))
+    # how long frame 1's MBs wait at group boundaries (wait phase at bx % 4 == 0)
+    wt = (st[1, :, :, 1] - st[1, :, :, 0]) / 100.0
+    print(f"frame 1 wait phase: at group starts mean {wt[:, 0::4].mean():.1f} us, elsewhere "
+          f"{np.delete(wt, np.s_[0::4], axis=1).mean():.1f} us")
+# deblock chunk k (MB k) publish vs the coding of MB k (stamp 9)
+for j in (0, 1):
+    for r in (3, 10, 20, hb - 1):
+        ks_ = [k for k in (2, 20, 40, 60) if k < wb]
+        print(f"  frame {j} row {r}: deblock chunk publish - MB(k) coded, us: " + "  ".join(
+            f"k={k}: {(dbs[j, r, k] - st[j, r, k, 9]) / 100.0:.1f}" for k in ks_))
+# frame 1, row 10: per group, when its inter task became ready / was claimed / done,
+# and when the row coder reached / resumed at the group's first MB
+if B > 1 and hb > 13 and (ist[..., 2] > 0).any():
+    r = 10
+    print(f"frame 1 row {r} per group (us): ready(deblock f0 row {r + 3}) claim done | coder reach resume")
+    for g in range(0, (wb + 3) // 4, 3):
+        need = min(64 * g + 96, w)
+        kk = [k for k in range(min(wb, 256)) if (16 * (k + 1) - 12 >= need or k == wb - 1)]
+        ready = (dbs[0, min(r + 3, hb - 1), kk[0]] - t0) / 100.0 if kk else float("nan")
+        c, dn = (ist[1, r, g, 0, 0] - t0) / 100.0, (ist[1, r, g, 0, 2] - t0) / 100.0
+        reach, res = (st[1, r, 4 * g, 0] - t0) / 100.0, (st[1, r, 4 * g, 1] - t0) / 100.0
+        print(f"  g={g:2d}: {ready:8.1f} {c:8.1f} {dn:8.1f} | {reach:8.1f} {res:8.1f}")
