@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--entropy-threads", type=int, default=8)
     p.add_argument("--no-end-to-end", action="store_true")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
-    p.add_argument("--batch", type=int, default=8, help="frames per engine launch (pipelined)")
+    p.add_argument("--batch", type=int, default=16, help="frames per engine launch (pipelined)")
     return p.parse_args()
 
 

@@ -28,9 +28,9 @@ using namespace cairo;
 
 namespace {
 
-constexpr int kStages = 16;      // staging slots (frames in flight)
+constexpr int kStages = 32;      // staging slots (frames in flight)
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
-constexpr int kDefaultBatch = 8;
+constexpr int kDefaultBatch = 16;
 constexpr int kSuccess = 0, kInvalidArg = 2, kOutOfMemory = 3, kHardwareFail = 5,
               kInvalidResource = 8;
 
