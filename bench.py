@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--steps", type=int, default=120)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="720p", choices=sorted(CONFIGS))
-    p.add_argument("--cpu-frames", type=int, default=48, help="P-frames in the bounded CPU baseline sample")
+    p.add_argument("--cpu-frames", type=int, default=0,
+                   help="P-frames in the bounded CPU baseline sample (0 = about 60 Mpixels: 10-20 s of one core)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--entropy-threads", type=int, default=8)
     p.add_argument("--no-end-to-end", action="store_true")
@@ -208,7 +209,8 @@ def main():
         "end_to_end": e2e,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, a.cpu_frames)
+        nf = a.cpu_frames or max(2, min(48, int(60e6 / (w * h))))
+        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, nf)
     else:
         result["cpu_baseline"] = None
     if rank == 0:

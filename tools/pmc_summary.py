@@ -23,7 +23,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHORT = {"k_convert": "convert", "k_inter_search": "inter_search", "k_mb_rows": "mb_rows"}
+SHORT = {"k_convert_batch": "convert", "k_engine": "engine"}
 
 
 def per_kernel(path):
@@ -33,7 +33,7 @@ def per_kernel(path):
         for k, short in SHORT.items():
             if f"::{k}(" in name:
                 vals.setdefault(short, []).append(float(r["Counter_Value"]))
-    # drop the first dispatch of each kernel (frame 0: intra, cold)
+    # drop the first dispatch of each kernel (warm-up: intra frame, cold caches)
     return {k: v[1:] if len(v) > 1 else v for k, v in vals.items()}
 
 
@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--round", default="r01")
     ap.add_argument("--config", default="720p")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--batch", type=int, default=16, help="frames per engine launch in the profiled run")
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
@@ -52,14 +53,18 @@ def main():
     write = per_kernel(os.path.join(a.src, "prof_write", "run_counter_collection.csv"))
     res = {"config": a.config, "round": a.round,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py; "
-                     "KiB per dispatch, median over P-frame dispatches; HBM bytes = 2*FETCH_SIZE (gfx950 "
-                     "correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE. Infinity-Cache hits are counted.",
-           "fetch_kib_raw": {}, "write_kib": {}, "per_launch_hbm_bytes": {}, "dispatches": {}}
+                     "KiB per dispatch, median over dispatches after the first; HBM bytes = 2*FETCH_SIZE (gfx950 "
+                     "correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE; per frame = per launch / frames per launch. "
+                     "Infinity-Cache hits are counted.",
+           "frames_per_launch": a.batch,
+           "fetch_kib_raw": {}, "write_kib": {}, "per_launch_hbm_bytes": {}, "per_frame_hbm_bytes": {},
+           "dispatches": {}}
     for k in sorted(set(fetch) & set(write)):
         f, w = statistics.median(fetch[k]), statistics.median(write[k])
         res["fetch_kib_raw"][k] = f
         res["write_kib"][k] = w
         res["per_launch_hbm_bytes"][k] = int(round((2 * f + w) * 1024))
+        res["per_frame_hbm_bytes"][k] = int(round((2 * f + w) * 1024 / a.batch))
         res["dispatches"][k] = min(len(fetch[k]), len(write[k]))
     path = os.path.join(out_dir, f"pmc_{a.config}.json")
     json.dump(res, open(path, "w"), indent=1)
