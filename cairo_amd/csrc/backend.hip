@@ -31,6 +31,8 @@ namespace {
 constexpr int kStages = 32;      // staging slots (frames in flight)
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
 constexpr int kDefaultBatch = 16;
+constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
+constexpr int kMaxLaunchWG = 240;  // workgroups per launch: two launches stay co-resident (2 per CU)
 constexpr int kSuccess = 0, kInvalidArg = 2, kOutOfMemory = 3, kHardwareFail = 5,
               kInvalidResource = 8;
 
@@ -58,7 +60,12 @@ struct cairo_ctx {
   uint32_t w = 0, h = 0, wa = 0, ha = 0, wmb = 0, hmb = 0, ring = 0;
   size_t plane_elems = 0, mbs = 0, nref = 1;
   hipStream_t ks = nullptr, cs = nullptr;
+  hipStream_t ks2 = nullptr;         // launches alternate between ks and ks2 (consecutive batches overlap)
   hipEvent_t engine_done = nullptr;  // last launched batch finished (copy stream waits on it)
+  hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k
+  hipEvent_t area_ready[kSyncAreas] = {}; // the launch using area k has zeroed it
+  long long batches = 0;             // launches so far
+  int prev_nframes = 0;              // frames of the previous launch
   // per-slot device buffers
   int16_t *src = nullptr, *coef = nullptr;
   BlockDesc *table = nullptr, *idesc = nullptr;
@@ -142,6 +149,7 @@ void free_ctx(cairo_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->ks) (void)hipStreamSynchronize(c->ks);
+  if (c->ks2) (void)hipStreamSynchronize(c->ks2);
   if (c->cs) (void)hipStreamSynchronize(c->cs);
   for (auto& s : c->st) {
     if (s.table) (void)hipHostFree(s.table);
@@ -153,6 +161,10 @@ void free_ctx(cairo_ctx* c) {
     for (auto& e : t.ev)
       if (e) (void)hipEventDestroy(e);
   if (c->engine_done) (void)hipEventDestroy(c->engine_done);
+  for (auto& ev : c->batch_end)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->area_ready)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
   for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad,
@@ -160,6 +172,7 @@ void free_ctx(cairo_ctx* c) {
                   (void*)c->predeblock, (void*)c->stamps})
     (void)hipFree(p);
   if (c->ks) (void)hipStreamDestroy(c->ks);
+  if (c->ks2) (void)hipStreamDestroy(c->ks2);
   if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
 }
@@ -204,20 +217,36 @@ int flush(cairo_ctx* c) {
   FrameArgs* fh = c->fdesc_host + (size_t)fslot * kMaxBatch;
   FrameArgs* fd = c->fdesc + (size_t)fslot * kMaxBatch;
   bool any_inter = false;
-  for (int i = 0; i < c->npend; i++) {
-    fh[i] = make_frame_view(e, c->pend[i], i);
-    any_inter |= fh[i].inter != 0;
-  }
+  for (int i = 0; i < c->npend; i++) any_inter |= c->pend[i].inter && c->ring > 1;
   e.fa = fd;
   const int rows = e.nframes * e.hmb;
   const int ng = (e.wmb + 3) / 4;
-  // Residency: 2 workgroups per CU (VGPRs), 256 CUs.  Every row has a coder
-  // and a helper (inter search + deblock) living as long as the row: equal pools.
   (void)any_inter;
-  (void)ng;
-  e.n_rows = c->wg_rows > 0 ? c->wg_rows : 240;
+  // Launch b alternates streams and sync areas; it follows launch b-1, which
+  // may still be running: its frame 0 reads the deblock progress of b-1's last
+  // frame.  Residency: 2 workgroups per CU (VGPRs) x 256 CUs = 512; a launch
+  // takes at most 240 so that two launches are always co-resident.  Every row
+  // has a coder and a helper (inter search + deblock) living as long as the
+  // row: equal pools.
+  const long long b = c->batches++;
+  hipStream_t st = (b & 1) ? c->ks2 : c->ks;
+  const int area = (int)(b % kSyncAreas);
+  e.sync = c->sync + (size_t)area * c->sync_words;
+  e.prev_last_deblocked =
+      b > 0 ? c->sync + (size_t)((b - 1) % kSyncAreas) * c->sync_words +
+                  SyncLayout::deblocked((int)c->hmb, ng, c->prev_nframes - 1)
+            : nullptr;
+  for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
+  c->prev_nframes = e.nframes;
+  e.n_rows = c->wg_rows > 0 ? c->wg_rows : kMaxLaunchWG / 2;
   if (e.n_rows > rows) e.n_rows = rows;
   e.n_helpers = e.n_rows;
+  // this sync area was last used by launch b-3 and read by launch b-2
+  if (b >= 2) CK(hipStreamWaitEvent(st, c->batch_end[(b - 2) % kSyncAreas], 0));
+  if (b >= 3) CK(hipStreamWaitEvent(st, c->batch_end[(b - 3) % kSyncAreas], 0));
+  // ...and this launch reads launch b-1's area: b-1 must have zeroed it first
+  // (otherwise the words still say "done" from launch b-4)
+  if (b >= 1) CK(hipStreamWaitEvent(st, c->area_ready[(b - 1) % kSyncAreas], 0));
   TimedBatch* tb = nullptr;
   if (c->profiling) {
     tb = &c->tb[c->tb_next];
@@ -225,28 +254,33 @@ int flush(cairo_ctx* c) {
     int r = collect_times(c, *tb);  // its events are about to be reused
     if (r) return r;
   }
-  CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, c->ks));
-  CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t), c->ks));
+  for (int i = 0; i < e.nframes; i++)  // host RGB sources
+    if (c->pend[i].host_rgb)
+      CK(hipMemcpyAsync((void*)c->pend[i].rgb, c->pend[i].host_rgb, (size_t)c->w * c->h * 3,
+                        hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, st));
+  CK(hipMemsetAsync(e.sync, 0, c->sync_words * sizeof(int32_t), st));
+  CK(hipEventRecord(c->area_ready[area], st));
   if (c->stamps) {  // engine entry (min) / exit (max) words
     static const uint64_t init[2] = {~0ull, 0};
     CK(hipMemcpyAsync(c->stamps + kMaxBatch * stamp_frame_words((int)c->wmb, (int)c->hmb), init, sizeof(init),
-                      hipMemcpyHostToDevice, c->ks));
+                      hipMemcpyHostToDevice, st));
   }
-  if (tb) CK(hipEventRecord(tb->ev[0], c->ks));
-  CK(launch_convert_batch(e, c->ks));
-  if (tb) CK(hipEventRecord(tb->ev[1], c->ks));
-  if (tb) CK(hipEventRecord(tb->ev[2], c->ks));
-  CK(launch_engine(e, c->ks));
+  if (tb) CK(hipEventRecord(tb->ev[0], st));
+  CK(launch_convert_batch(e, st));
+  if (tb) CK(hipEventRecord(tb->ev[1], st));
+  if (tb) CK(hipEventRecord(tb->ev[2], st));
+  CK(launch_engine(e, st));
   if (tb) {
-    CK(hipEventRecord(tb->ev[3], c->ks));
+    CK(hipEventRecord(tb->ev[3], st));
     tb->frames = e.nframes;
     tb->pending = true;
   }
   const int last = c->pend[e.nframes - 1].slot;
-  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), c->ks));
+  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
   // outputs for the host entropy stage, on the copy stream
-  CK(hipEventRecord(c->engine_done, c->ks));
-  CK(hipStreamWaitEvent(c->cs, c->engine_done, 0));
+  CK(hipEventRecord(c->batch_end[area], st));
+  CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
   for (int i = 0; i < e.nframes; i++) {
     const int slot = c->pend[i].slot;
     Stage& s = c->st[slot];
@@ -267,6 +301,7 @@ int sync_all(cairo_ctx* c) {
   int r = flush(c);
   if (r) return r;
   CK(hipStreamSynchronize(c->ks));
+  CK(hipStreamSynchronize(c->ks2));
   CK(hipStreamSynchronize(c->cs));
   return kSuccess;
 }
@@ -311,6 +346,7 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   } while (0)
   TRY(hipSetDevice(device));
   TRY(hipStreamCreateWithFlags(&c->ks, hipStreamNonBlocking));
+  TRY(hipStreamCreateWithFlags(&c->ks2, hipStreamNonBlocking));
   TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
   TRY(hipMalloc(&c->src, c->plane_elems * 2 * kStages));
   TRY(hipMalloc(&c->coef, c->plane_elems * 2 * kStages));
@@ -320,7 +356,7 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * kStages));
   TRY(hipMalloc(&c->gran, c->mbs * kGranuleStride * sizeof(uint64_t) * kStages));
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * kStages));
-  TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t)));
+  TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t) * kSyncAreas));
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
   {  // (frame, row) task order of the engine pools, for every batch size
@@ -349,6 +385,8 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   for (auto& t : c->tb)
     for (auto& e : t.ev) TRY(hipEventCreate(&e));
   TRY(hipEventCreateWithFlags(&c->engine_done, hipEventDisableTiming));
+  for (auto& ev : c->batch_end) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (auto& ev : c->area_ready) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 #undef TRY
   r = zero_state(c);
   if (r != kSuccess) {
@@ -428,10 +466,10 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   FrameDesc& f = c->pend[c->npend];
   if (rgb_on_device) {
     f.rgb = rgb;
-  } else {
-    uint8_t* dst = c->rgb + (size_t)slot * c->w * c->h * 3;
-    CK(hipMemcpyAsync(dst, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, c->ks));
-    f.rgb = dst;
+    f.host_rgb = nullptr;
+  } else {  // uploaded at launch, on the launch's stream (the caller keeps it valid until wait)
+    f.rgb = c->rgb + (size_t)slot * c->w * c->h * 3;
+    f.host_rgb = rgb;
   }
   f.index = (int)index;
   f.inter = type == 1 ? 1 : 0;

@@ -50,6 +50,7 @@ constexpr int kMaxBatch = 16;
 // One frame of a batch (host-filled, kernarg).
 struct FrameDesc {
   const uint8_t* rgb;  // RGB888, pitch 3*w (device memory)
+  const uint8_t* host_rgb;  // host source to upload into rgb at launch (nullptr: already on device)
   int index;           // frame index (common.cpp:192-195 ring addressing)
   int inter;           // 0 intra, 1 inter (references 1..R-1)
   int quality;         // 1..31
@@ -123,7 +124,9 @@ struct EngineArgs {
   int32_t* isad_base;      // stride nref * mbs
   uint64_t* gran_base;     // stride mbs * kGranuleStride
   int16_t* ring_base;      // R reconstruction slots, stride plane_elems
-  int32_t* sync;           // SyncLayout words
+  int32_t* sync;           // SyncLayout words of this launch
+  const int32_t* prev_last_deblocked;  // deblock progress words of the frame before frame 0,
+                                       // if it belongs to a launch that may still run (else nullptr)
   int32_t* sticky;
   uint64_t* stamps;
   int n_helpers, n_rows;   // worker pools (workgroups); blockIdx order: helpers, rows

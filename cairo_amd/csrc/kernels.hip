@@ -1589,7 +1589,7 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.nref = a.inter ? e.ring - 1 : 1;
   a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, a.ng, j);
   a.deblocked = e.sync + SyncLayout::deblocked(e.hmb, a.ng, j);
-  a.prev_deblocked = j > 0 ? e.sync + SyncLayout::deblocked(e.hmb, a.ng, j - 1) : nullptr;
+  a.prev_deblocked = j > 0 ? e.sync + SyncLayout::deblocked(e.hmb, a.ng, j - 1) : e.prev_last_deblocked;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   a.rgb = f.rgb;
   return a;

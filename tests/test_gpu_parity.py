@@ -217,8 +217,10 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0):
     final_slots = [e.planes(2 + k) for k in range(ring)]
     ctx = cairo.Context(w, h, ring)
     ctx.set_batch(batch)
-    tickets = [ctx.submit(orc.make_frame(w, h, t), t, not ref[t][0], q) for t in range(frames)]
-    for t, tk in enumerate(tickets):
+    stages = ctx.L.cairo_ctx_stages(ctx.h)
+    pending = []
+
+    def check(t, tk):
         out = ctx.wait(tk)
         tag = f"{w}x{h} R={ring} q={q} batch={batch} frame {t}"
         _table_equal(out.table, ref[t][1], f"{tag}: block table")
@@ -226,6 +228,13 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0):
         np.testing.assert_array_equal(out.coef_u, ref[t][2][1], err_msg=f"{tag}: coef U")
         np.testing.assert_array_equal(out.coef_v, ref[t][2][2], err_msg=f"{tag}: coef V")
         ctx.release(tk)
+
+    for t in range(frames):  # at most `stages` frames in flight (submitted, not released)
+        if len(pending) == stages:
+            check(*pending.pop(0))
+        pending.append((t, ctx.submit(orc.make_frame(w, h, t), t, not ref[t][0], q)))
+    for p in pending:
+        check(*p)
     ctx.sync()
     for k in range(ring):
         gy, gu, gv = ctx.read_planes(2 + k)
@@ -251,3 +260,14 @@ def test_batched_720p(orc, cairo):
 def test_batched_ragged(orc, cairo):
     _run_batched(orc, cairo, 200, 120, 3, 16, 9, 4)
     _run_batched(orc, cairo, 16, 16, 2, 16, 6, 6)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 16])
+def test_overlapping_launches_long(orc, cairo, batch):
+    """Many launches in flight (consecutive launches overlap on two streams):
+    40 CIF frames, R=2, an intra frame every 11th."""
+    _run_batched(orc, cairo, 352, 288, 2, 16, 40, batch, intra_every=11)
+
+
+def test_overlapping_launches_720p(orc, cairo):
+    _run_batched(orc, cairo, 1280, 720, 2, 16, 20, 4)
