@@ -1515,7 +1515,7 @@ __device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds&
 // deadlock with every workgroup resident.
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_engine(EngineArgs e) {
+__global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   __shared__ EngineLds L;
   const int b = blockIdx.x, hmb = e.hmb;
   uint64_t* ks = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, hmb) : nullptr;
