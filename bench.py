@@ -262,16 +262,23 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, 
 
 def run_e2e(ctx, frame_ptr, first, count, q, stages, entropy, pending):
     inflight = deque()
+    nxt = None  # ticket of the next submission (tickets are consecutive)
     for f in range(first, first + count):
-        # a staging slot is free once its entropy job released it
-        while len(inflight) + len(pending) >= stages:
-            if inflight:
+        # ticket T reuses the staging slot of ticket T - stages, which is free
+        # once that ticket's entropy job released it (jobs finish out of order)
+        while inflight or pending:
+            cands = ([inflight[0]] if inflight else []) + ([min(pending)] if pending else [])
+            oldest = min(cands)
+            if nxt is None or nxt - oldest < stages:
+                break
+            if inflight and inflight[0] == oldest:
                 t = inflight.popleft()
                 entropy(t, ctx.wait(t, copy=False))
             else:
-                k = next(iter(pending))
-                pending.pop(k).result()
-        inflight.append(ctx.submit(frame_ptr(f), f, f > 0, q, on_device=True))
+                pending.pop(oldest).result()
+        t = ctx.submit(frame_ptr(f), f, f > 0, q, on_device=True)
+        inflight.append(t)
+        nxt = t + 1
     while inflight:
         t = inflight.popleft()
         entropy(t, ctx.wait(t, copy=False))

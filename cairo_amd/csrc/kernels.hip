@@ -939,8 +939,15 @@ __device__ __forceinline__ void deblock_task(const FrameArgs& a, int r, DbLds& D
 // frame's tag".
 // ---------------------------------------------------------------------------
 
-constexpr int kCwLP = 130;  // luma window pitch (elements): 128 columns, odd dword stride
-constexpr int kCwCP = 66;   // chroma window pitch: 64 columns
+// Window storage: values are biased (v ^ 0x8000) so that unsigned 16-bit
+// order equals signed order (reconstructions are unclamped int16, SURVEY.md
+// Appendix A.4), which lets the candidate search use packed u16 instructions.
+// Columns are circular (x & 127, chroma x & 63); the first 16 (4) columns are
+// repeated after the last so that a row read never wraps.  Pitches: 74 / 37
+// dwords, so the 16 rows a candidate group reads hit 16 distinct banks.
+constexpr int kCwLP = 148;  // luma pitch (elements): 128 + 16-column tail + pad
+constexpr int kCwCP = 74;   // chroma pitch: 64 + 4-column tail + pad
+constexpr int kLumaTail = 16, kChromaTail = 4;
 
 struct alignas(16) RowWindow {
   int16_t y[80 * kCwLP];
@@ -955,22 +962,52 @@ struct alignas(16) RowLds {
   int32_t red[12];
 };
 
-// Dword k (0..191) of macroblock (mbx, mby): its address in plane set p and in
-// the window (same order as the granules, kernels.h).
+// Pixel pair (int16 lo = column col, hi = col+1; col even) of plane pl at
+// window row `row`.
+__device__ __forceinline__ void win_put2(RowWindow& w, int pl, int row, int col, uint32_t pair) {
+  const uint32_t b = pair ^ 0x80008000u;
+  if (pl == 0) {
+    const int c = col & 127;
+    *(uint32_t*)&w.y[row * kCwLP + c] = b;
+    if (c < kLumaTail) *(uint32_t*)&w.y[row * kCwLP + 128 + c] = b;
+  } else {
+    int16_t* t = pl == 1 ? w.u : w.v;
+    const int c = col & 63;
+    *(uint32_t*)&t[row * kCwCP + c] = b;
+    if (c < kChromaTail) *(uint32_t*)&t[row * kCwCP + 64 + c] = b;
+  }
+}
+__device__ __forceinline__ void win_put1(RowWindow& w, int pl, int row, int col, int v) {
+  const int16_t b = (int16_t)(v ^ 0x8000);
+  if (pl == 0) {
+    const int c = col & 127;
+    w.y[row * kCwLP + c] = b;
+    if (c < kLumaTail) w.y[row * kCwLP + 128 + c] = b;
+  } else {
+    int16_t* t = pl == 1 ? w.u : w.v;
+    const int c = col & 63;
+    t[row * kCwCP + c] = b;
+    if (c < kChromaTail) t[row * kCwCP + 64 + c] = b;
+  }
+}
+__device__ __forceinline__ int unbias(int16_t b) { return (int)(int16_t)(b ^ (int16_t)0x8000); }
+
+// Dword k (0..191) of macroblock (mbx, mby): its address in plane set p (same
+// order as the granules, kernels.h), and its store into the window.
 __device__ __forceinline__ const int16_t* win_src(const PlaneSet& p, int wa, int mbx, int mby, int k) {
   if (k < 128) return p.y + (size_t)(mby * 16 + (k >> 3)) * wa + mbx * 16 + 2 * (k & 7);
   const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
   return pick(p, 1 + pl) + (size_t)(mby * 8 + r) * (wa >> 1) + mbx * 8 + 2 * d;
 }
-__device__ __forceinline__ uint32_t* win_dst(RowWindow& w, int oy, int mbx, int mby, int k) {
+__device__ __forceinline__ void win_put_k(RowWindow& w, int oy, int mbx, int mby, int k, uint32_t pair) {
   if (k < 128) {
-    const int gy = mby * 16 + (k >> 3), gx = mbx * 16 + 2 * (k & 7);
-    return (uint32_t*)&w.y[(gy - oy) * kCwLP + (gx & 127)];
+    win_put2(w, 0, mby * 16 + (k >> 3) - oy, mbx * 16 + 2 * (k & 7), pair);
+  } else {
+    const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
+    win_put2(w, 1 + pl, mby * 8 + r - (oy >> 1), mbx * 8 + 2 * d, pair);
   }
-  const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
-  const int gy = mby * 8 + r, gx = mbx * 8 + 2 * d;
-  return (uint32_t*)&(pl ? w.v : w.u)[(gy - (oy >> 1)) * kCwCP + (gx & 63)];
 }
+
 // Sum / max over one 16-lane DPP row (a candidate's group); all 16 lanes get it.
 __device__ __forceinline__ int row16_sum(int v) {
   v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
@@ -988,31 +1025,52 @@ __device__ __forceinline__ int row16_max(int v) {
 }
 
 // A 16-lane group evaluates one candidate: lane i owns luma row i (16 px) and
-// 4 pixels of U and V (row i>>1, columns (i&1)*4..+3).
+// 4 pixels of U and V (row i>>1, columns (i&1)*4..+3).  Source pixels as
+// biased u16 pairs.
 struct SrcRow {
-  int y[16], u[4], v[4];
+  uint32_t y[8], u[2], v[2];
 };
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ int src_px(const uint32_t* p, int k) {  // unbiased pixel k
+  return unbias((int16_t)(p[k >> 1] >> (16 * (k & 1))));
+}
+
+// |src - cand| over biased pairs: SAD (v_sad_u16) and the two one-sided
+// saturated differences, whose packed maxima give the MAD.
+__device__ __forceinline__ void pk_diff(uint32_t a, uint32_t b, uint32_t& sad, u16x2& m1, u16x2& m2) {
+  sad = __builtin_amdgcn_sad_u16(a, b, sad);
+  m1 = __builtin_elementwise_max(m1, __builtin_elementwise_sub_sat(as_u16x2(a), as_u16x2(b)));
+  m2 = __builtin_elementwise_max(m2, __builtin_elementwise_sub_sat(as_u16x2(b), as_u16x2(a)));
+}
 
 __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int cy, int i,
                                          const SrcRow& s, int& sad, int& mad) {
-  const int16_t* row = &w.y[(cy + i - oy) * kCwLP];
-  int sm = 0, mx = 0;
+  uint32_t sm = 0;
+  u16x2 m1 = {0, 0}, m2 = {0, 0};
+  {
+    const int c = cx & 127, sh = (c & 1) * 2;
+    const uint32_t* row = (const uint32_t*)&w.y[(cy + i - oy) * kCwLP] + (c >> 1);
+    uint32_t d[9];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int d = abs(s.y[k] - row[(cx + k) & 127]);
-    sm += d;
-    mx = max(mx, d);
-  }
-  const int cr = (cy >> 1) + (i >> 1) - (oy >> 1), cc = (cx >> 1) + (i & 1) * 4;
-  const int16_t* ru = &w.u[cr * kCwCP];
-  const int16_t* rv = &w.v[cr * kCwCP];
+    for (int k = 0; k < 9; k++) d[k] = row[k];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    mx = max(mx, abs(s.u[k] - ru[(cc + k) & 63]));
-    mx = max(mx, abs(s.v[k] - rv[(cc + k) & 63]));
+    for (int k = 0; k < 8; k++) pk_diff(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), sm, m1, m2);
   }
-  sad = row16_sum(sm);
-  mad = row16_max(mx);
+  {
+    const int cr = (cy >> 1) + (i >> 1) - (oy >> 1), cc = ((cx >> 1) + (i & 1) * 4) & 63, sh = (cc & 1) * 2;
+    const uint32_t* ru = (const uint32_t*)&w.u[cr * kCwCP] + (cc >> 1);
+    const uint32_t* rv = (const uint32_t*)&w.v[cr * kCwCP] + (cc >> 1);
+    const uint32_t u0 = ru[0], u1 = ru[1], u2 = ru[2], v0 = rv[0], v1 = rv[1], v2 = rv[2];
+    uint32_t dummy = 0;
+    pk_diff(s.u[0], __builtin_amdgcn_alignbyte(u1, u0, sh), dummy, m1, m2);
+    pk_diff(s.u[1], __builtin_amdgcn_alignbyte(u2, u1, sh), dummy, m1, m2);
+    pk_diff(s.v[0], __builtin_amdgcn_alignbyte(v1, v0, sh), dummy, m1, m2);
+    pk_diff(s.v[1], __builtin_amdgcn_alignbyte(v2, v1, sh), dummy, m1, m2);
+  }
+  const u16x2 m = __builtin_elementwise_max(m1, m2);
+  sad = row16_sum((int)sm);
+  mad = row16_max(max((int)m.x, (int)m.y));
 }
 
 // Sub-pel candidate: lerp of the best block (bx, by) toward neighbour (tx, ty).
@@ -1024,7 +1082,7 @@ __device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, i
   int sm = 0, mx = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int d = abs(s.y[k] - lerp_px(ra[(bx + k) & 127], rb[(tx + k) & 127], q));
+    const int d = abs(src_px(s.y, k) - lerp_px(unbias(ra[(bx + k) & 127]), unbias(rb[(tx + k) & 127]), q));
     sm += d;
     mx = max(mx, d);
   }
@@ -1032,10 +1090,10 @@ __device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, i
   const int xa = (bx >> 1) + (i & 1) * 4, xb = (tx >> 1) + (i & 1) * 4;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    mx = max(mx, abs(s.u[k] - lerp_px(w.u[ca * kCwCP + ((xa + k) & 63)],
-                                      w.u[cb * kCwCP + ((xb + k) & 63)], q)));
-    mx = max(mx, abs(s.v[k] - lerp_px(w.v[ca * kCwCP + ((xa + k) & 63)],
-                                      w.v[cb * kCwCP + ((xb + k) & 63)], q)));
+    mx = max(mx, abs(src_px(s.u, k) - lerp_px(unbias(w.u[ca * kCwCP + ((xa + k) & 63)]),
+                                              unbias(w.u[cb * kCwCP + ((xb + k) & 63)]), q)));
+    mx = max(mx, abs(src_px(s.v, k) - lerp_px(unbias(w.v[ca * kCwCP + ((xa + k) & 63)]),
+                                              unbias(w.v[cb * kCwCP + ((xb + k) & 63)]), q)));
   }
   sad = row16_sum(sm);
   mad = row16_max(mx);
@@ -1048,9 +1106,9 @@ __device__ __forceinline__ bool intra_valid(int cx, int cy, int px, int py, int 
 
 // Pixel (ex, ey) of plane pl (0 Y, 1 U, 2 V) from the window.
 __device__ __forceinline__ int win_px(const RowWindow& w, int oy, int pl, int ex, int ey) {
-  if (pl == 0) return w.y[(ey - oy) * kCwLP + (ex & 127)];
+  if (pl == 0) return unbias(w.y[(ey - oy) * kCwLP + (ex & 127)]);
   const int16_t* t = pl == 1 ? w.u : w.v;
-  return t[(ey - (oy >> 1)) * kCwCP + (ex & 63)];
+  return unbias(t[(ey - (oy >> 1)) * kCwCP + (ex & 63)]);
 }
 
 __device__ __forceinline__ const int16_t* plane_of(const PlaneSet& p, int pl) {
@@ -1147,24 +1205,27 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
           for (int k = tid; k < n * kGranulesPerMB; k += 256) {
             const int i = k / kGranulesPerMB, kk = k - i * kGranulesPerMB;
             const uint64_t* gp = gran_at(a, lx[i], ly[i], kk);
-            *win_dst(L.win, oy, lx[i], ly[i], kk) = gran_settle(gp, gran_ld(gp), tag, err, a.sticky);
+            win_put_k(L.win, oy, lx[i], ly[i], kk, gran_settle(gp, gran_ld(gp), tag, err, a.sticky));
           }
         } else if (bx + 2 < a.wmb && tid < kGranulesPerMB) {
           const uint64_t* gp = gran_at(a, bx + 2, by - 1, tid);
-          *win_dst(L.win, oy, bx + 2, by - 1, tid) = gran_settle(gp, gran_ld(gp), tag, err, a.sticky);
+          win_put_k(L.win, oy, bx + 2, by - 1, tid, gran_settle(gp, gran_ld(gp), tag, err, a.sticky));
         }
       }
       // source rows of this lane's group slot
-      SrcRow s;
+      SrcRow s;  // biased u16 pairs
       {
-        const int8v r0 = load_row8(a.in.y + (size_t)(py + gi) * a.wa + px);
-        const int8v r1 = load_row8(a.in.y + (size_t)(py + gi) * a.wa + px + 8);
-#pragma unroll
-        for (int k = 0; k < 8; k++) s.y[k] = r0[k], s.y[8 + k] = r1[k];
+        const uint4* ry = (const uint4*)(a.in.y + (size_t)(py + gi) * a.wa + px);
+        const uint4 r0 = ry[0], r1 = ry[1];
+        s.y[0] = r0.x, s.y[1] = r0.y, s.y[2] = r0.z, s.y[3] = r0.w;
+        s.y[4] = r1.x, s.y[5] = r1.y, s.y[6] = r1.z, s.y[7] = r1.w;
         const size_t co = (size_t)((py >> 1) + (gi >> 1)) * cw + (px >> 1) + (gi & 1) * 4;
-        const short4 u4 = *(const short4*)(a.in.u + co), v4 = *(const short4*)(a.in.v + co);
-        s.u[0] = u4.x, s.u[1] = u4.y, s.u[2] = u4.z, s.u[3] = u4.w;
-        s.v[0] = v4.x, s.v[1] = v4.y, s.v[2] = v4.z, s.v[3] = v4.w;
+        const uint2 u2 = *(const uint2*)(a.in.u + co), v2 = *(const uint2*)(a.in.v + co);
+        s.u[0] = u2.x, s.u[1] = u2.y, s.v[0] = v2.x, s.v[1] = v2.y;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s.y[k] ^= 0x80008000u;
+#pragma unroll
+        for (int k = 0; k < 2; k++) s.u[k] ^= 0x80008000u, s.v[k] ^= 0x80008000u;
       }
       const bool pf3 = by >= 3 && bx + 3 < a.wmb, pf2 = by >= 2 && bx + 3 < a.wmb;
       const bool pfs = by + 1 < a.hmb && bx + 1 < a.wmb;
@@ -1205,7 +1266,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
       {
         int sm = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) sm += abs(s.y[k]);
+        for (int k = 0; k < 16; k++) sm += abs(src_px(s.y, k));
         sel.sad = uni(row16_sum(sm));  // compute_block_sad(src): every group holds the total
       }
       sel.bx = px;
@@ -1347,19 +1408,16 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
         const int b = wave + 4 * bi, e = b * 64 + lane;
         int pl, ex, ey;
         elem_coords(e, px, py, pl, ex, ey);
-        if (pl == 0)
-          L.win.y[(ey - oy) * kCwLP + (ex & 127)] = (int16_t)pv[bi];
-        else
-          (pl == 1 ? L.win.u : L.win.v)[(ey - (oy >> 1)) * kCwCP + (ex & 63)] = (int16_t)pv[bi];
+        win_put1(L.win, pl, pl == 0 ? ey - oy : ey - (oy >> 1), ex, pv[bi]);
       }
       if (tid < kGranulesPerMB) {  // prefetched window blocks for MB bx+1
         if (pf3)
-          *win_dst(L.win, oy, bx + 3, by - 3, tid) =
-              gran_settle(gran_at(a, bx + 3, by - 3, tid), pg3, tag, err, a.sticky);
+          win_put_k(L.win, oy, bx + 3, by - 3, tid,
+                    gran_settle(gran_at(a, bx + 3, by - 3, tid), pg3, tag, err, a.sticky));
         if (pf2)
-          *win_dst(L.win, oy, bx + 3, by - 2, tid) =
-              gran_settle(gran_at(a, bx + 3, by - 2, tid), pg2, tag, err, a.sticky);
-        if (pfs) *win_dst(L.win, oy, bx, by + 1, tid) = pst;
+          win_put_k(L.win, oy, bx + 3, by - 2, tid,
+                    gran_settle(gran_at(a, bx + 3, by - 2, tid), pg2, tag, err, a.sticky));
+        if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
       if (tid == 0) a.table[mb] = d;
       stamp(a, mb, 8);

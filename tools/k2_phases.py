@@ -98,7 +98,7 @@ if B > 2:
     print(f"frame 1 wait phase: at group starts mean {wt[:, 0::4].mean():.1f} us, elsewhere "
           f"{np.delete(wt, np.s_[0::4], axis=1).mean():.1f} us")
 # deblock chunk k (MB k) publish vs the coding of MB k (stamp 9)
-for j in (0, 1):
+for j in range(min(B, 2)):
     for r in (3, 10, 20, hb - 1):
         ks_ = [k for k in (2, 20, 40, 60) if k < wb]
         print(f"  frame {j} row {r}: deblock chunk publish - MB(k) coded, us: " + "  ".join(
