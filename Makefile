@@ -3,7 +3,7 @@
 HIPCC   ?= /opt/rocm/bin/hipcc
 CXX     = g++
 ARCH    ?= gfx950
-CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+CXXFLAGS = -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-function
 HIPFLAGS = --offload-arch=$(ARCH) $(CXXFLAGS) -munsafe-fp-atomics
 SRC      = cairo_amd/csrc
 OBJ      = build/obj
@@ -11,7 +11,7 @@ LIB      = cairo_amd/_lib/libcairo_amd.so
 ORACLE   = oracle/liboracle.so
 
 HIP_SRCS = $(SRC)/kernels.hip $(SRC)/backend.hip
-CPP_SRCS = $(SRC)/entropy.cpp $(SRC)/bitstream.cpp $(SRC)/encoder.cpp $(SRC)/decoder.cpp
+CPP_SRCS = $(SRC)/entropy.cpp $(SRC)/bitstream.cpp $(SRC)/encoder.cpp $(SRC)/decoder.cpp $(SRC)/pipeline.cpp
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
 HDRS     = $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
 

@@ -21,7 +21,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 from collections import deque
 
@@ -49,7 +48,8 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=0,
                    help="P-frames in the bounded CPU baseline sample (0 = about 60 Mpixels: 10-20 s of one core)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--entropy-threads", type=int, default=8)
+    p.add_argument("--entropy-threads", type=int, default=0,
+                   help="entropy workers per rank (0: min(14, host CPUs / ranks - 2); the GPU box gives 16 CPUs per GPU)")
     p.add_argument("--no-end-to-end", action="store_true")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
     p.add_argument("--batch", type=int, default=16, help="frames per engine launch (pipelined)")
@@ -221,69 +221,38 @@ def main():
 
 
 def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, world):
-    """Hot path + host entropy (frames spread over threads), bitstreams produced."""
-    import concurrent.futures as cf
-
+    """Hot path + host entropy through the native frame pipeline
+    (cairo_stream_*: entropy on a pool of C++ worker threads); every frame's
+    payload is appended to one output buffer (bitstream produced)."""
     stages = ctx.L.cairo_ctx_stages(ctx.h)
-    pool = cf.ThreadPoolExecutor(max_workers=a.entropy_threads)
-    pending = {}
-    bits = {}
-    lock = threading.Lock()
+    if a.entropy_threads <= 0:
+        a.entropy_threads = max(1, min(14, (os.cpu_count() or 4) // world - 2))
+    st = cairo_amd.Stream(ctx, threads=a.entropy_threads)
+    out = np.zeros(max(w * h * 4, 1 << 20), np.uint8)  # payload bits of the frames in flight, reused
 
-    def entropy(t, out):
-        # serialize_slice releases the GIL (ctypes) while it runs
-        def job(t=t, out=out):
-            _, n = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, out.coef_y, out.coef_u, out.coef_v)
-            with lock:
-                bits[t] = n
-            ctx.release(t)
+    def run(first, count):
+        inflight = deque()
+        pos = 0
+        for f in range(first, first + count):
+            if len(inflight) == stages:
+                pos = st.collect(inflight.popleft(), out, 0)
+            inflight.append(st.submit(frame_ptr(f), f, f > 0, q, on_device=True))
+        while inflight:
+            pos = st.collect(inflight.popleft(), out, 0)
+        return pos
 
-        pending[t] = pool.submit(job)
-        # bound in-flight entropy work to the staging depth
-        done = [k for k, fut in pending.items() if fut.done()]
-        for k in done:
-            pending.pop(k).result()
-
-    # warmup (I + P) then timed P-frames
-    run_e2e(ctx, frame_ptr, 0, a.warmup, q, stages, entropy, pending)
+    run(0, a.warmup)  # I + P warmup
     barrier()
     t0 = time.perf_counter()
-    run_e2e(ctx, frame_ptr, a.warmup, a.steps, q, stages, entropy, pending)
-    ctx.sync()
+    run(a.warmup, a.steps)
     barrier()
     el = time.perf_counter() - t0
-    pool.shutdown(wait=True)
+    st.close()
     el = max_over_ranks(el, dist, dev)
     return {"value": round(aggregate_mpix(w, h, a.steps, world, el), 3), "unit": "Mpix/s",
             "ms_per_step": round(el * 1e3 / a.steps, 4), "entropy_threads": a.entropy_threads,
             "staging_slots": stages,
-            "note": "hot path + host entropy (serialize_slice) pipelined; bitstreams produced"}
-
-
-def run_e2e(ctx, frame_ptr, first, count, q, stages, entropy, pending):
-    inflight = deque()
-    nxt = None  # ticket of the next submission (tickets are consecutive)
-    for f in range(first, first + count):
-        # ticket T reuses the staging slot of ticket T - stages, which is free
-        # once that ticket's entropy job released it (jobs finish out of order)
-        while inflight or pending:
-            cands = ([inflight[0]] if inflight else []) + ([min(pending)] if pending else [])
-            oldest = min(cands)
-            if nxt is None or nxt - oldest < stages:
-                break
-            if inflight and inflight[0] == oldest:
-                t = inflight.popleft()
-                entropy(t, ctx.wait(t, copy=False))
-            else:
-                pending.pop(oldest).result()
-        t = ctx.submit(frame_ptr(f), f, f > 0, q, on_device=True)
-        inflight.append(t)
-        nxt = t + 1
-    while inflight:
-        t = inflight.popleft()
-        entropy(t, ctx.wait(t, copy=False))
-    for k in list(pending):
-        pending.pop(k).result()
+            "note": "hot path + host entropy (native frame pipeline, cairo_stream_*); payload bits produced"}
 
 
 def cpu_baseline(cairo_amd, w, h, ring, q, pframes):

@@ -80,6 +80,11 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_set_batch": (I, [P, I]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
+        "cairo_stream_create": (I, [P, I, ctypes.POINTER(P)]),
+        "cairo_stream_submit": (I, [P, P, I, U, U, U, ctypes.POINTER(I)]),
+        "cairo_stream_collect": (I, [P, I, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+        "cairo_stream_destroy": (I, [P]),
+        "cairo_bits_append": (I, [P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), P, ctypes.c_uint64]),
         "evx_encoder_create": (I, [ctypes.POINTER(P)]),
         "evx_encoder_destroy": (I, [P]),
         "evx_encoder_clear": (I, [P]),
@@ -291,6 +296,65 @@ def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv
     )
     n = pos.value
     return out[: (n + 7) // 8].tobytes(), n
+
+
+def bits_append(dst: np.ndarray, pos: int, src: bytes, nbits: int) -> int:
+    """Append nbits of src (LSB-first) at bit pos of the uint8 array dst -> new pos."""
+    p = ctypes.c_uint64(pos)
+    s = np.frombuffer(src, np.uint8) if len(src) else np.zeros(1, np.uint8)
+    _ck(lib().cairo_bits_append(_ptr(dst), dst.size * 8, ctypes.byref(p), _ptr(s), nbits), "cairo_bits_append")
+    return p.value
+
+
+class Stream:
+    """Frame pipeline (``cairo_stream_*``): GPU hot path + host entropy on
+    native worker threads.  Drives ``ctx`` exclusively while open."""
+
+    def __init__(self, ctx: "Context", threads: int = 0):
+        self.L = lib()
+        self.ctx = ctx
+        p = ctypes.c_void_p()
+        _ck(self.L.cairo_stream_create(ctx.h, threads, ctypes.byref(p)), "cairo_stream_create")
+        self.h = p
+        self._keep = {}
+
+    def submit(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> int:
+        t = ctypes.c_int()
+        ptr = rgb if on_device else _ptr(rgb)
+        _ck(self.L.cairo_stream_submit(self.h, ptr, int(on_device), index, int(inter), quality, ctypes.byref(t)),
+            "cairo_stream_submit")
+        if not on_device:
+            self._keep[t.value] = rgb
+        return t.value
+
+    def collect(self, ticket: int, out: np.ndarray | None = None, pos: int = 0):
+        """Append the frame's payload at bit pos of out -> new pos; with out
+        None, return (bytes, nbits) of the payload alone."""
+        if out is None:
+            p = ctypes.c_uint64(0)
+            # size query is not separate: collect into a buffer large enough for any frame
+            buf = np.zeros(self.ctx.wa * self.ctx.ha * 8 + 65536, np.uint8)
+            _ck(self.L.cairo_stream_collect(self.h, ticket, _ptr(buf), buf.size, ctypes.byref(p)),
+                "cairo_stream_collect")
+            self._keep.pop(ticket, None)
+            return buf[: (p.value + 7) // 8].tobytes(), p.value
+        p = ctypes.c_uint64(pos)
+        _ck(self.L.cairo_stream_collect(self.h, ticket, _ptr(out), out.size, ctypes.byref(p)), "cairo_stream_collect")
+        self._keep.pop(ticket, None)
+        return p.value
+
+    def close(self) -> None:
+        if self.h:
+            r = self.L.cairo_stream_destroy(self.h)
+            self.h = None
+            self._keep.clear()
+            _ck(r, "cairo_stream_destroy")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class BitStream:

@@ -16,12 +16,15 @@
 // while the GPU runs the next batch).
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
 #include "../../include/cairo_amd.h"
+#include "ctx_internal.h"
 #include "kernels.h"
 
 using namespace cairo;
@@ -96,6 +99,12 @@ struct cairo_ctx {
   int acc_frames = 0;
   int16_t* predeblock = nullptr;  // debug: pre-deblock reconstruction of the last frame (opt-in)
   uint64_t* stamps = nullptr;     // diagnostic phase stamps (opt-in)
+  // Thread safety (the frame pipeline of pipeline.cpp calls in from its
+  // completion and entropy threads): every public entry point holds mu;
+  // HIP event waits on a frame's outputs run outside it.  launched_cv is
+  // signalled when a batch launches.
+  std::mutex mu;
+  std::condition_variable launched_cv;
 };
 
 namespace {
@@ -294,6 +303,7 @@ int flush(cairo_ctx* c) {
   }
   c->last_slot = last;
   c->npend = 0;
+  c->launched_cv.notify_all();
   return kSuccess;
 }
 
@@ -405,6 +415,7 @@ int cairo_ctx_destroy(cairo_ctx* c) {
 
 int cairo_ctx_reset(cairo_ctx* c) {
   if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);
   if (r) return r;
@@ -416,6 +427,7 @@ int cairo_ctx_stages(const cairo_ctx*) { return kStages; }
 
 int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
   if (!c || frames < 1 || frames > kMaxBatch || frames > kStages / 2) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   int r = flush(c);
   if (r) return r;
   c->batch_max = frames;
@@ -424,18 +436,21 @@ int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
 
 int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
   if (!c || rows < 0) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   c->wg_rows = rows;
   return kSuccess;
 }
 
 int cairo_ctx_set_profiling(cairo_ctx* c, int enable) {
   if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   c->profiling = enable != 0;
   return kSuccess;
 }
 
 int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
   if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = flush(c);
   if (r) return r;
@@ -455,6 +470,7 @@ int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
 int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32_t index,
                      uint32_t type, uint32_t quality, int* ticket) {
   if (!c || !rgb || !ticket || quality < 1 || quality > 31 || type > 1) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   const int t = c->next_ticket;
   const int slot = t % kStages;
@@ -490,15 +506,9 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   return kSuccess;
 }
 
-int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
-  if (!c || !out || ticket < 0) return kInvalidArg;
-  Stage& s = c->st[ticket % kStages];
-  if (!s.busy || s.ticket != ticket) return kInvalidResource;
+// Frame outputs once its D2H finished (called without mu held).
+static int frame_result(cairo_ctx* c, Stage& s, cairo_frame_result* out) {
   CK(hipSetDevice(c->device));
-  if (!s.launched) {
-    int r = flush(c);
-    if (r) return r;
-  }
   CK(hipEventSynchronize(s.d2h_done));
   if (*s.err) {
     fprintf(stderr, "[cairo_amd] an in-kernel wait timed out (at or before frame %u)\n", s.index);
@@ -518,8 +528,24 @@ int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
   return kSuccess;
 }
 
+int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
+  if (!c || !out || ticket < 0) return kInvalidArg;
+  Stage& s = c->st[ticket % kStages];
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!s.busy || s.ticket != ticket) return kInvalidResource;
+    CK(hipSetDevice(c->device));
+    if (!s.launched) {
+      int r = flush(c);
+      if (r) return r;
+    }
+  }
+  return frame_result(c, s, out);
+}
+
 int cairo_ctx_release(cairo_ctx* c, int ticket) {
   if (!c || ticket < 0) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   Stage& s = c->st[ticket % kStages];
   if (s.ticket != ticket) return kInvalidResource;
   s.busy = false;
@@ -528,12 +554,14 @@ int cairo_ctx_release(cairo_ctx* c, int ticket) {
 
 int cairo_ctx_sync(cairo_ctx* c) {
   if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   return sync_all(c);
 }
 
 int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16_t* v) {
   if (!c || which < 0 || which >= 2 + (int)c->ring) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);
   if (r) return r;
@@ -550,6 +578,7 @@ int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16
 
 int cairo_ctx_read_inter(cairo_ctx* c, uint8_t* descs, int32_t* sads) {
   if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);
   if (r) return r;
@@ -564,6 +593,7 @@ int cairo_ctx_read_inter(cairo_ctx* c, uint8_t* descs, int32_t* sads) {
 
 int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
   if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = flush(c);
   if (r) return r;
@@ -586,6 +616,7 @@ int cairo_ctx_read_trace(cairo_ctx* c, int32_t* out, int n) {
 
 int cairo_ctx_read_stamps(cairo_ctx* c, uint64_t* out) {
   if (!c || !c->stamps || !out) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);
   if (r) return r;
@@ -595,6 +626,7 @@ int cairo_ctx_read_stamps(cairo_ctx* c, uint64_t* out) {
 
 int cairo_ctx_read_predeblock(cairo_ctx* c, int16_t* y, int16_t* u, int16_t* v) {
   if (!c || !c->predeblock) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);
   if (r) return r;
@@ -608,6 +640,7 @@ int cairo_ctx_read_predeblock(cairo_ctx* c, int16_t* y, int16_t* u, int16_t* v) 
 
 int cairo_ctx_read_table(cairo_ctx* c, uint8_t* table) {
   if (!c || !table) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);
   if (r) return r;
@@ -661,3 +694,42 @@ int cairo_device_count(void) {
 const char* cairo_version(void) { return "cairo_amd 0.1 (gfx950)"; }
 
 }  // extern "C"
+
+namespace cairo {
+
+int ctx_wait_launched(cairo_ctx* c, int ticket, const std::atomic<bool>* stop,
+                      cairo_frame_result* out) {
+  if (!c || !out || ticket < 0) return kInvalidArg;
+  Stage& s = c->st[ticket % kStages];
+  {
+    std::unique_lock<std::mutex> lk(c->mu);
+    if (!s.busy || s.ticket != ticket) return kInvalidResource;
+    c->launched_cv.wait(lk, [&] { return s.launched || (stop && stop->load()); });
+    if (!s.launched) return kInvalidResource;
+  }
+  return frame_result(c, s, out);
+}
+
+int ctx_flush(cairo_ctx* c) {
+  if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  CK(hipSetDevice(c->device));
+  return flush(c);
+}
+
+void ctx_wake(cairo_ctx* c) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->launched_cv.notify_all();
+}
+
+int ctx_geometry(cairo_ctx* c, uint32_t* wmb, uint32_t* hmb, uint32_t* ring, int* next_ticket) {
+  if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *next_ticket = c->next_ticket;
+  *wmb = c->wmb;
+  *hmb = c->hmb;
+  *ring = c->ring;
+  return kSuccess;
+}
+
+}  // namespace cairo

@@ -115,6 +115,34 @@ CAIRO_API int cairo_serialize_slice(const uint8_t *block_table, uint32_t wmb, ui
                                     const int16_t *coef_v, uint8_t *out, uint32_t out_bytes,
                                     uint32_t *bit_pos);
 
+/* ---- frame pipeline ---------------------------------
+ * GPU hot path + host entropy for a stream of frames: the caller submits
+ * frames, a completion thread picks up each frame's outputs, a pool of entropy
+ * workers runs serialize_slice on them in parallel (frames are
+ * entropy-independent: the ABAC model restarts per slice, serialize.cpp:323),
+ * and collect appends a frame's payload bits.  Appending the frame descriptors
+ * and payloads in ticket order yields the reference stream (evx1enc.cpp:119-168).
+ * The stream drives ctx exclusively while it exists (no direct cairo_ctx_submit
+ * / wait / release); destroy it before the context.  A host RGB source must
+ * stay valid until its frame is collected. */
+typedef struct cairo_stream cairo_stream;
+/* threads: entropy workers (0 = hardware threads - 1, at most 15). */
+CAIRO_API int cairo_stream_create(cairo_ctx *ctx, int threads, cairo_stream **out);
+/* Blocks while the frame's staging slot (ticket - stages) is still being
+ * entropy-coded; EVX_ERROR_INVALID_RESOURCE (8) if ticket - 2*stages has not
+ * been collected. */
+CAIRO_API int cairo_stream_submit(cairo_stream *s, const uint8_t *rgb, int rgb_on_device,
+                                  uint32_t index, uint32_t type, uint32_t quality, int *ticket);
+/* Wait for the frame's payload and append it at bit *bit_pos of out
+ * (out_bytes capacity, LSB-first; out == NULL only advances *bit_pos). */
+CAIRO_API int cairo_stream_collect(cairo_stream *s, int ticket, uint8_t *out, uint64_t out_bytes,
+                                   uint64_t *bit_pos);
+/* Finish all submitted frames and stop the threads. */
+CAIRO_API int cairo_stream_destroy(cairo_stream *s);
+/* Append n bits of src at bit *pos of dst (cap_bits), bit_stream semantics. */
+CAIRO_API int cairo_bits_append(uint8_t *dst, uint64_t cap_bits, uint64_t *pos, const uint8_t *src,
+                                uint64_t n);
+
 /* ---- drop-in encoder, C view of evx1_encoder (evx1.h:66-94) ------------- */
 CAIRO_API int evx_encoder_create(void **enc);
 CAIRO_API int evx_encoder_destroy(void *enc);

@@ -54,3 +54,28 @@ def test_entropy_random_tables(orc, cairo):
     a = cairo.serialize_slice(table, wmb, hmb, 4, y, u, v)
     b = cairo.serialize_slice(table.copy(), wmb, hmb, 4, y.copy(), u.copy(), v.copy())
     assert a == b and a[1] > 0
+
+
+def _bits(buf: bytes, n: int):
+    return [(buf[i >> 3] >> (i & 7)) & 1 for i in range(n)]
+
+
+def test_bits_append_matches_bitwise_model(cairo):
+    """cairo_bits_append (frame-pipeline collect): appending payloads at any
+    bit offset == writing them bit by bit; bits past the end stay untouched
+    (bit_stream semantics, bitstream.cpp:181-245)."""
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        dst = rng.integers(0, 256, 64, dtype=np.uint8)
+        before = dst.copy()
+        pos = int(rng.integers(0, 200))
+        n = int(rng.integers(0, 250))
+        src = rng.integers(0, 256, (n + 7) // 8 + 1, dtype=np.uint8).tobytes()
+        new = cairo.bits_append(dst, pos, src, n)
+        assert new == pos + n
+        got = _bits(dst.tobytes(), 512)
+        want = _bits(before.tobytes(), 512)
+        want[pos:pos + n] = _bits(src, n)
+        assert got == want, (pos, n)
+    with pytest.raises(cairo.CairoError):
+        cairo.bits_append(np.zeros(2, np.uint8), 10, b"\xff\xff", 7)

@@ -9,6 +9,7 @@ frozen stream hashes in tests/golden/oracle_streams.json (themselves pinned
 to the reference's recorded sizes, tests/test_oracle.py).
 """
 import json
+import struct
 import os
 
 import numpy as np
@@ -271,3 +272,86 @@ def test_overlapping_launches_long(orc, cairo, batch):
 
 def test_overlapping_launches_720p(orc, cairo):
     _run_batched(orc, cairo, 1280, 720, 2, 16, 20, 4)
+
+
+# ---------------------------------------------------------------------------
+# Frame pipeline (cairo_stream_*): GPU hot path + native entropy workers.
+# Frame records assembled from its payloads must reproduce the reference
+# stream (evx1enc.cpp:119-168 order: [header], frame desc, payload).
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("cfg", STREAMS, ids=[c["name"] for c in STREAMS])
+def test_stream_matches_golden(orc, cairo, cfg):
+    w, h, ring, q = cfg["width"], cfg["height"], cfg["ring"], cfg["quality"]
+    ctx = cairo.Context(w, h, ring)
+    ctx.set_batch(4)
+    st = cairo.Stream(ctx, threads=3)
+    frames = [cairo.make_band4(w, h, t) for t in range(cfg["frames"])]
+    tks = [st.submit(f, t, not (cfg["intra_only"] or t == 0), q) for t, f in enumerate(frames)]
+    hsh = orc.FNV_OFFSET
+    for t, tk in enumerate(tks):
+        typ = 0 if (cfg["intra_only"] or t == 0) else 1
+        hdr = struct.pack("<4sHBxHHH", b"EVX1", 14, ring, (2 << 8) | 47, w, h) if t == 0 else b""
+        head = hdr + struct.pack("<IIH", typ, t, q)
+        buf = np.zeros(len(head) + w * h * 8, np.uint8)
+        buf[: len(head)] = np.frombuffer(head, np.uint8)
+        n = st.collect(tk, buf, len(head) * 8)
+        assert n == cfg["frame_bits"][t], f"frame {t}"
+        hsh = orc.fnv1a64(orc.canonical_frame_bytes(buf.tobytes(), n, t == 0), hsh)
+    assert f"{hsh:016x}" == cfg["fnv1a64"]
+    st.close()
+    ctx.close()
+
+
+def test_stream_long_unaligned(orc, cairo):
+    """90 CIF frames (more than 2 x stages in flight over time), R=2, intra
+    every 11th, payloads appended back to back at unaligned bit offsets into
+    one buffer; every frame record equals the oracle encoder's."""
+    w, h, ring, q, n = 352, 288, 2, 16, 90
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    ctx = cairo.Context(w, h, ring)
+    st = cairo.Stream(ctx, threads=4)
+    stages = ctx.L.cairo_ctx_stages(ctx.h)
+    out = np.zeros(n * w * h, np.uint8)
+    pos = 0
+    inflight = []
+    ref = []
+    for t in range(n):
+        intra = t % 11 == 0
+        if intra:
+            e.insert_intra()
+        rgb = orc.make_frame(w, h, t)
+        data, nb = e.encode(rgb)
+        ref.append((data, nb, intra))
+        if len(inflight) == stages:
+            tt, tk = inflight.pop(0)
+            pos = _append_record(st, out, pos, tt, tk, ref, w, h, ring, q)
+        inflight.append((t, st.submit(rgb, t, not intra, q)))
+    for tt, tk in inflight:
+        pos = _append_record(st, out, pos, tt, tk, ref, w, h, ring, q)
+    # the concatenated records, frame by frame
+    p = 0
+    for t, (data, nb, _) in enumerate(ref):
+        want = np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[:nb]
+        got = np.unpackbits(out, bitorder="little")[p:p + nb]
+        if t == 0:  # header pad byte 7
+            want = want.copy()
+            got = got.copy()
+            want[56:64] = 0
+            got[56:64] = 0
+        np.testing.assert_array_equal(got, want, err_msg=f"frame {t}")
+        p += nb
+    assert p == pos
+    st.close()
+    ctx.close()
+
+
+def _append_record(st, out, pos, t, tk, ref, w, h, ring, q):
+    intra = ref[t][2]
+    hdr = struct.pack("<4sHBxHHH", b"EVX1", 14, ring, (2 << 8) | 47, w, h) if t == 0 else b""
+    head = hdr + struct.pack("<IIH", 0 if intra else 1, t, q)
+    import cairo_amd
+
+    pos = cairo_amd.bits_append(out, pos, head, len(head) * 8)
+    return st.collect(tk, out, pos)
