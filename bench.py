@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=120)
+    p.add_argument("--steps", type=int, default=300, help="timed P-frames (BASELINE configs: 300-frame IPPP streams)")
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="720p", choices=sorted(CONFIGS))
     p.add_argument("--cpu-frames", type=int, default=0,
@@ -230,28 +230,40 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, 
     st = cairo_amd.Stream(ctx, threads=a.entropy_threads)
     out = np.zeros(max(w * h * 4, 1 << 20), np.uint8)  # payload bits of the frames in flight, reused
 
+    tl = []
+
+    def collect(tk):
+        st.collect(tk, out, 0)
+        tl.append(st.timeline(tk))
+
     def run(first, count):
         inflight = deque()
-        pos = 0
         for f in range(first, first + count):
             if len(inflight) == stages:
-                pos = st.collect(inflight.popleft(), out, 0)
+                collect(inflight.popleft())
             inflight.append(st.submit(frame_ptr(f), f, f > 0, q, on_device=True))
         while inflight:
-            pos = st.collect(inflight.popleft(), out, 0)
-        return pos
+            collect(inflight.popleft())
 
     run(0, a.warmup)  # I + P warmup
     barrier()
     t0 = time.perf_counter()
+    tl.clear()
     run(a.warmup, a.steps)
     barrier()
     el = time.perf_counter() - t0
     st.close()
     el = max_over_ranks(el, dist, dev)
+    T = np.array(tl)  # per frame: submitted, outputs on host, entropy start/end, collected (us)
+    mid = T[len(T) // 4: 3 * len(T) // 4]
+    pipeline = {
+        "latency_submit_to_outputs_ms": round(float(np.mean(T[:, 1] - T[:, 0])) / 1e3, 3),
+        "entropy_ms_per_frame_per_thread": round(float(np.mean(T[:, 3] - T[:, 2])) / 1e3, 3),
+        "steady_period_ms_per_frame": round(float(np.mean(np.diff(mid[:, 4]))) / 1e3, 4),
+    }
     return {"value": round(aggregate_mpix(w, h, a.steps, world, el), 3), "unit": "Mpix/s",
             "ms_per_step": round(el * 1e3 / a.steps, 4), "entropy_threads": a.entropy_threads,
-            "staging_slots": stages,
+            "staging_slots": stages, "pipeline": pipeline,
             "note": "hot path + host entropy (native frame pipeline, cairo_stream_*); payload bits produced"}
 
 

@@ -84,6 +84,7 @@ def lib() -> ctypes.CDLL:
         "cairo_stream_submit": (I, [P, P, I, U, U, U, ctypes.POINTER(I)]),
         "cairo_stream_collect": (I, [P, I, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
         "cairo_stream_destroy": (I, [P]),
+        "cairo_stream_timeline": (I, [P, I, P]),
         "cairo_bits_append": (I, [P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), P, ctypes.c_uint64]),
         "evx_encoder_create": (I, [ctypes.POINTER(P)]),
         "evx_encoder_destroy": (I, [P]),
@@ -342,6 +343,12 @@ class Stream:
         _ck(self.L.cairo_stream_collect(self.h, ticket, _ptr(out), out.size, ctypes.byref(p)), "cairo_stream_collect")
         self._keep.pop(ticket, None)
         return p.value
+
+    def timeline(self, ticket: int):
+        """(submitted, outputs on host, entropy start, entropy end, collected), us."""
+        t = (ctypes.c_double * 5)()
+        _ck(self.L.cairo_stream_timeline(self.h, ticket, t), "cairo_stream_timeline")
+        return list(t)
 
     def close(self) -> None:
         if self.h:

@@ -14,8 +14,9 @@ namespace cairo {
 // ctx_wake after setting it).
 int ctx_wait_launched(cairo_ctx* c, int ticket, const std::atomic<bool>* stop,
                       cairo_frame_result* out);
-// Launch the pending (partial) batch.
-int ctx_flush(cairo_ctx* c);
+// Launch the pending (partial) batch; with ticket >= 0 only if that frame is
+// part of it (not yet launched).
+int ctx_flush(cairo_ctx* c, int ticket = -1);
 void ctx_wake(cairo_ctx* c);
 // Macroblock grid, ring size and the ticket the next submit will get.
 int ctx_geometry(cairo_ctx* c, uint32_t* wmb, uint32_t* hmb, uint32_t* ring, int* next_ticket);

@@ -22,7 +22,9 @@
 // reference stream (tests/test_gpu_parity.py::test_stream_*).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -38,8 +40,18 @@ namespace {
 
 constexpr int kSuccess = 0, kInvalidArg = 2, kCapacityLimit = 7, kInvalidResource = 8;
 
+double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Per-frame timeline (us, steady clock): submitted, outputs on the host
+// (completion thread), entropy start, entropy end, collected.
+enum { kTSubmit, kTOutputs, kTEntropy0, kTEntropy1, kTCollect, kTimes };
+
 struct Frame {
   enum State { kFree, kSubmitted, kDone };
+  double t[kTimes] = {};
   int ticket = -1;
   State state = kFree;
   int status = kSuccess;
@@ -67,6 +79,7 @@ struct cairo_stream {
   std::atomic<bool> stop{false};
   std::thread completer;
   std::vector<std::thread> workers;
+  bool skip_entropy = false;  // diagnostic (CAIRO_STREAM_SKIP_ENTROPY=1): plumbing only, empty payloads
 
   Frame& at(int t) { return fr[(size_t)t % fr.size()]; }
   void finish(int t, int status, uint64_t nbits) {
@@ -99,6 +112,7 @@ struct cairo_stream {
       }
       {
         std::lock_guard<std::mutex> lk(m);
+        at(t).t[kTOutputs] = now_us();
         jobs.push_back(j);
       }
       cv.notify_all();
@@ -116,12 +130,17 @@ struct cairo_stream {
         jobs.pop_front();
       }
       Frame& f = at(j.ticket);  // owned by this worker until kDone
+      f.t[kTEntropy0] = now_us();
       const cairo_frame_result& o = j.res;
       if (f.bits.empty()) f.bits.resize(std::max<size_t>((size_t)o.wa * o.ha / 2, 1 << 16));
       uint64_t pos = 0;
       int r;
       for (;;) {
         pos = 0;
+        if (skip_entropy) {
+          r = kSuccess;
+          break;
+        }
         r = cairo::serialize_slice(o.block_table, wmb, hmb, ring, o.coef_y, o.coef_u, o.coef_v,
                                    f.bits.data(), (uint64_t)f.bits.size() * 8, &pos);
         // a frame's precode is bounded by the feed capacity per section, so
@@ -129,6 +148,7 @@ struct cairo_stream {
         if (r != kCapacityLimit || f.bits.size() >= ((size_t)1 << 31)) break;
         f.bits.resize(f.bits.size() * 2);
       }
+      f.t[kTEntropy1] = now_us();
       cairo_ctx_release(ctx, j.ticket);
       finish(j.ticket, r, pos);
     }
@@ -191,6 +211,8 @@ int cairo_stream_create(cairo_ctx* ctx, int threads, cairo_stream** out) {
     return r;
   }
   s->fr.resize((size_t)2 * s->stages);
+  const char* skip = getenv("CAIRO_STREAM_SKIP_ENTROPY");
+  s->skip_entropy = skip && skip[0] == '1';
   if (threads <= 0) {
     const unsigned hw = std::thread::hardware_concurrency();
     threads = (int)std::min(15u, hw > 1 ? hw - 1 : 1u);
@@ -223,6 +245,7 @@ int cairo_stream_submit(cairo_stream* s, const uint8_t* rgb, int rgb_on_device, 
     std::lock_guard<std::mutex> lk(s->m);
     Frame& f = s->at(tk);
     f.ticket = tk;
+    f.t[kTSubmit] = now_us();
     f.state = Frame::kSubmitted;
     f.status = kSuccess;
     f.nbits = 0;
@@ -244,8 +267,8 @@ int cairo_stream_collect(cairo_stream* s, int ticket, uint8_t* out, uint64_t out
     if (f.ticket != ticket || f.state == Frame::kFree) return kInvalidResource;
     pending = f.state == Frame::kSubmitted;
   }
-  if (pending) {  // its batch may not be launched yet
-    const int r = cairo::ctx_flush(s->ctx);
+  if (pending) {  // launch its batch if it is still the pending one
+    const int r = cairo::ctx_flush(s->ctx, ticket);
     if (r) return r;
   }
   {
@@ -261,10 +284,20 @@ int cairo_stream_collect(cairo_stream* s, int ticket, uint8_t* out, uint64_t out
   }
   {
     std::lock_guard<std::mutex> lk(s->m);
+    f.t[kTCollect] = now_us();
     f.state = Frame::kFree;
   }
   s->cv.notify_all();
   return r;
+}
+
+int cairo_stream_timeline(cairo_stream* s, int ticket, double* t) {
+  if (!s || !t || ticket < 0) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(s->m);
+  const Frame& f = s->at(ticket);
+  if (f.ticket != ticket) return kInvalidResource;
+  for (int k = 0; k < kTimes; k++) t[k] = f.t[k];
+  return kSuccess;
 }
 
 int cairo_stream_destroy(cairo_stream* s) {

@@ -137,6 +137,10 @@ CAIRO_API int cairo_stream_submit(cairo_stream *s, const uint8_t *rgb, int rgb_o
  * (out_bytes capacity, LSB-first; out == NULL only advances *bit_pos). */
 CAIRO_API int cairo_stream_collect(cairo_stream *s, int ticket, uint8_t *out, uint64_t out_bytes,
                                    uint64_t *bit_pos);
+/* Diagnostic timeline of a collected frame (valid until ticket + 2*stages is
+ * submitted): t[5] = submitted, outputs on the host, entropy start, entropy
+ * end, collected; microseconds of a monotonic clock. */
+CAIRO_API int cairo_stream_timeline(cairo_stream *s, int ticket, double *t);
 /* Finish all submitted frames and stop the threads. */
 CAIRO_API int cairo_stream_destroy(cairo_stream *s);
 /* Append n bits of src at bit *pos of dst (cap_bits), bit_stream semantics. */
