@@ -1402,6 +1402,23 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
         }
       }
       stamp(a, mb, 7);
+      // publish first (the next row's coder waits for exactly these): pixel
+      // pairs (lane, lane^1) of each 8x8 block as granules.  No drain before
+      // them: the coefficient stores only have to be visible to whoever
+      // observes the info granule below (the deblock, and through its
+      // progress the next frame's copy macroblocks), which is stored after
+      // the drain.
+      _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+        const int b = wave + 4 * bi;
+        const int nb = __builtin_amdgcn_mov_dpp(pv[bi], 0xB1, 0xF, 0xF, false);  // lane ^ 1
+        if (!(lane & 1)) {
+          const int r = lane >> 3, c2 = (lane & 7) >> 1;
+          const int k = b < 4 ? (((b >> 1) * 8 + r) * 8 + (b & 1) * 4 + c2) : (128 + (b - 4) * 32 + r * 4 + c2);
+          gran_st(gran_at(a, bx, by, k),
+                  ((uint64_t)tag << 32) | ((uint32_t)pv[bi] & 0xFFFFu) | ((uint32_t)nb << 16));
+        }
+      }
+      stamp(a, mb, 8);
       // reconstruction -> the window (the slot is written by the deblock,
       // from the granules)
       _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
@@ -1420,22 +1437,14 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
       if (tid == 0) a.table[mb] = d;
-      stamp(a, mb, 8);
-      // publish: pixel pairs (lane, lane^1) of each 8x8 block as granules.
-      // Drain first: whoever observes these granules (and everything causally
-      // after) must also see this MB's write-through coefficient stores.
+      // every wave's coefficient stores drained, then the block info for the
+      // deblock (its edge strengths); thread 0's drain covers only wave 0, so
+      // the other waves drain before the barrier of the next macroblock --
+      // the deblock reads their coefficients only through this granule, hence
+      // the barrier: info after all four waves drained
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
-        const int b = wave + 4 * bi;
-        const int nb = __builtin_amdgcn_mov_dpp(pv[bi], 0xB1, 0xF, 0xF, false);  // lane ^ 1
-        if (!(lane & 1)) {
-          const int r = lane >> 3, c2 = (lane & 7) >> 1;
-          const int k = b < 4 ? (((b >> 1) * 8 + r) * 8 + (b & 1) * 4 + c2) : (128 + (b - 4) * 32 + r * 4 + c2);
-          gran_st(gran_at(a, bx, by, k),
-                  ((uint64_t)tag << 32) | ((uint32_t)pv[bi] & 0xFFFFu) | ((uint32_t)nb << 16));
-        }
-      }
-      if (tid == 0)  // block info for the deblock (its edge strengths)
+      __syncthreads();
+      if (tid == 0)
         gran_st(gran_at(a, bx, by, kGranulesPerMB),
                 ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index);
       stamp(a, mb, 9);

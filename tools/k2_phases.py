@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cairo_amd  # noqa: E402
 
 CFG = {"720p": (1280, 720, 2, 16), "1080p": (1920, 1080, 4, 8), "4k": (3840, 2160, 4, 16), "cif": (352, 288, 4, 16)}
-PHASES = ["wait", "window", "int_search", "subpel", "classify", "pred", "code", "store", "publish"]
+PHASES = ["wait", "window", "int_search", "subpel", "classify", "pred", "code", "publish", "window+drain"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="720p")
@@ -67,7 +67,7 @@ for j in range(B):
     for by in range(1, hb):
         for bx in range(wb):
             src = min(bx + 2, wb - 1)
-            lat.append((st[j, by, bx, 1] - st[j, by - 1, src, 9]) / 100.0)
+            lat.append((st[j, by, bx, 1] - st[j, by - 1, src, 8]) / 100.0)  # pixel granules out at stamp 8
 lat = np.array(lat)
 print(f"  hand-off (publish -> resume) mean {lat.mean():.3f} p50 {np.median(lat):.3f} us")
 clk = (st[..., 11] - st[..., 10]) / np.maximum(st[..., 9] - st[..., 0], 1) * 100.0  # MHz
