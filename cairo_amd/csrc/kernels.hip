@@ -235,20 +235,23 @@ struct alignas(16) Window {
   int16_t v[kWinC * kWinCP];
 };
 
-// Stage the in-frame part of the window with origin (ox, oy) (luma pixels,
+// Stage the in-frame part of window rows [r0, r1) x columns [c0, c1) (luma,
+// multiples of 16; chroma the halves) with origin (ox, oy) (luma pixels,
 // multiples of 16) from plane set p.  All 256 threads participate.
 __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa, int ha, int ox,
-                                            int oy) {
-  for (int k = threadIdx.x; k < kWinL * (kWinLW / 8); k += 256) {  // 16-B chunks
-    const int r = k >> 4, c = (k & 15) * 8;
+                                            int oy, int r0, int r1, int c0, int c1) {
+  const int nc = (c1 - c0) >> 3, nl = (r1 - r0) * nc;  // 16-B chunks per row / in all
+  for (int k = threadIdx.x; k < nl; k += 256) {
+    const int r = r0 + k / nc, c = c0 + (k % nc) * 8;
     const int gy = oy + r, gx = ox + c;
     if (gy >= 0 && gy < ha && gx >= 0 && gx < wa)
       *(int4*)&w.y[r * kWinLP + c] = *(const int4*)&p.y[(size_t)gy * wa + gx];
   }
   const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
-  for (int k = threadIdx.x; k < 2 * kWinC * (kWinCW / 8); k += 256) {
-    const int pl = k / (kWinC * 8), kk = k - pl * kWinC * 8;
-    const int r = kk >> 3, c = (kk & 7) * 8;
+  const int ncc = nc >> 1, ncl = ((r1 - r0) >> 1) * ncc;
+  for (int k = threadIdx.x; k < 2 * ncl; k += 256) {
+    const int pl = k >= ncl, kk = k - pl * ncl;
+    const int r = (r0 >> 1) + kk / ncc, c = (c0 >> 1) + (kk % ncc) * 8;
     const int gy = coy + r, gx = cox + c;
     if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
       const int16_t* src = pick(p, 1 + pl);
@@ -464,12 +467,93 @@ __device__ __forceinline__ BlockDesc make_desc(const Sel& s, int px, int py, int
 // `off`, one wave per macroblock, in the shared window.
 // ---------------------------------------------------------------------------
 
+// The window is staged in two levels.  Level 1, window rows [0, 64) x columns
+// [0, 112) (frame rows py-32..py+31, columns 64g-32..64g+79), covers the
+// zero-MV block, the whole first (+-16) step of every macroblock of the group
+// and any later candidate that stays there: it needs the previous frame final
+// on MB rows <= r+1 over those columns, i.e. its deblock progress of row r+2
+// (whose top edge finishes row r+1) at 64g+80.  Level 2 (the rest: the bottom
+// 16 rows and the right 16 columns) is staged only when a step could reach it,
+// after the previous frame's deblock progress of row r+3 passed 64g+96.  With
+// typical motion the search never leaves level 1, so a frame follows its
+// predecessor at MB rows r+2 / +5 macroblocks instead of r+3 / +6.
+constexpr int kLvl1Rows = 64, kLvl1Cols = 112;
+
+#ifndef CAIRO_HELPER_INTERLEAVE
+#define CAIRO_HELPER_INTERLEAVE 1
+#endif
+constexpr bool kHelperInterleave = CAIRO_HELPER_INTERLEAVE;
+
+// Thread 0's value v, broadcast to the workgroup (two barriers).
+__device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
+  if (threadIdx.x == 0) *slot = v;
+  __syncthreads();
+  const int r = *slot;
+  __syncthreads();
+  return r;
+}
+
+// The row's deblock (defined below), advanced while a helper waits.
+struct DbLds;
+struct DbState;
+__device__ __forceinline__ bool deblock_chunk_ready(const FrameArgs& a, int r, const DbState& st);
+__device__ __forceinline__ void deblock_chunk(const FrameArgs& a, int r, DbLds& D, DbState& st);
+__device__ __forceinline__ bool deblock_pending(const FrameArgs& a, const DbState& st);
+
+// Helper wait (whole workgroup): until the previous frame's deblock progress
+// of MB row rr reaches need, running this row's ready deblock chunks
+// meanwhile; then acquire what the progress word released.  Bounded like
+// every wait (the error word ends it).
+__device__ __forceinline__ void helper_wait(const FrameArgs& a, int r, int rr, int need, DbLds& D,
+                                            DbState& st, int* flag) {
+  volatile int* vflag = flag;
+  uint64_t t0 = 0;
+  for (;;) {
+    int d = 0;
+    if (threadIdx.x == 0) {
+      if (!a.prev_deblocked ||
+          __hip_atomic_load(a.prev_deblocked + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) {
+        d = 1;
+      } else if (kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
+        d = 2;
+      } else {  // nothing to do: back off
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (!t0) t0 = now;
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          d = 1;
+        } else if (now - t0 > 200000000ull) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          d = 1;
+        }
+      }
+    }
+    d = wg_broadcast(vflag, d);
+    if (d == 1) break;
+    if (d == 2) deblock_chunk(a, r, D, st);
+  }
+  if (threadIdx.x == 0) {  // the check used a relaxed load: acquire what it observed
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 struct InterLds {
   Window win;
   int need[4];
+  int lvl2[6][4];  // per step (16, 8, 4, 2, 1, sub-pel) and wave: level 2 wanted
 };
 
-__device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int off, InterLds& L) {
+// Need of the group's level-1 / level-2 windows: (MB row whose deblock
+// progress counts, luma columns).
+__device__ __forceinline__ int inter_need_cols(const FrameArgs& a, int g, int level) {
+  return min(64 * g + (level == 1 ? 80 : 96), a.wa);
+}
+
+__device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int off, InterLds& L, DbLds& D,
+                                           DbState& st, int* flag) {
   const int wave = threadIdx.x >> 6;
   const int x = 4 * g + wave;
   const bool valid = x < a.wmb;
@@ -493,10 +577,28 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
   __syncthreads();
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
     const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
-    load_window(L.win, ref, a.wa, a.ha, ox, oy);
+    load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, 0, kLvl1Cols);
     __syncthreads();
-    if (need) {
-      for (int step = kRadius; step > 0; step >>= 1) {
+    bool lvl2 = false;  // workgroup-uniform
+    // steps 16, 8, 4, 2, 1, then the sub-pel step (reach 1 around the best)
+    for (int si = 0; si < 6; si++) {
+      const int step = si < 5 ? kRadius >> si : 1;
+      if (!lvl2) {
+        // this wave's candidates of the step reach window rows by+step-oy+15
+        // and columns bx+step-ox+15 at most
+        const bool want = need && (s.by + step - oy > kLvl1Rows - kMB || s.bx + step - ox > kLvl1Cols - kMB);
+        if ((threadIdx.x & 63) == 0) L.lvl2[si][wave] = want;
+        __syncthreads();
+        if (L.lvl2[si][0] | L.lvl2[si][1] | L.lvl2[si][2] | L.lvl2[si][3]) {
+          helper_wait(a, r, min(r + 3, a.hmb - 1), inter_need_cols(a, g, 2), D, st, flag);
+          load_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
+          load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
+          __syncthreads();
+          lvl2 = true;
+        }
+      }
+      if (!need) continue;
+      if (si < 5) {
         const int bx = s.bx, by = s.by;
         for (int j = -step; j <= step; j += step)
           for (int i = -step; i <= step; i += step) {
@@ -506,24 +608,25 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
             sad_mad(src, px_from_window(L.win, cx - ox, cy - oy), sad, mad);
             accept_int(s, cx, cy, sad, mad, px, py, thr);
           }
-      }
-      // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
-      const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
-      s.sp_idx = s.sp_amt = s.sp_en = 0;
-      const int bx = s.bx, by = s.by;
-      for (int j = -1; j <= 1; j++)
-        for (int i = -1; i <= 1; i++) {
-          if (i == 0 && j == 0) continue;
-          const int tx = bx + i, ty = by + j;
-          if (!in_frame(tx, ty, a.wa, a.ha)) continue;
-          const Px6 nb = px_from_window(L.win, tx - ox, ty - oy);
-          const int idx = frac_index(i, j);
-          for (int q = 0; q < 2; q++) {
-            int sad, mad;
-            sad_mad(src, lerp6(best, nb, q), sad, mad);
-            accept_sub(s, idx, q, sad, mad, thr);
+      } else {
+        // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
+        const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
+        s.sp_idx = s.sp_amt = s.sp_en = 0;
+        const int bx = s.bx, by = s.by;
+        for (int j = -1; j <= 1; j++)
+          for (int i = -1; i <= 1; i++) {
+            if (i == 0 && j == 0) continue;
+            const int tx = bx + i, ty = by + j;
+            if (!in_frame(tx, ty, a.wa, a.ha)) continue;
+            const Px6 nb = px_from_window(L.win, tx - ox, ty - oy);
+            const int idx = frac_index(i, j);
+            for (int q = 0; q < 2; q++) {
+              int sad, mad;
+              sad_mad(src, lerp6(best, nb, q), sad, mad);
+              accept_sub(s, idx, q, sad, mad, thr);
+            }
           }
-        }
+      }
     }
   }
   if (valid && (threadIdx.x & 63) == 0) {
@@ -764,6 +867,10 @@ struct DbState {
 
 // Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
 // Evaluated by thread 0 only.
+__device__ __forceinline__ bool deblock_pending(const FrameArgs& a, const DbState& st) {
+  return st.k < (a.wa + kDbChunk - 1) / kDbChunk;
+}
+
 __device__ __forceinline__ bool deblock_chunk_ready(const FrameArgs& a, int r, const DbState& st) {
   const int c1 = min((st.k + 1) * kDbChunk, a.wa);
   if (r > 0 && __hip_atomic_load(&a.deblocked[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1)
@@ -1454,10 +1561,6 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
 }
 
 
-#ifndef CAIRO_HELPER_INTERLEAVE
-#define CAIRO_HELPER_INTERLEAVE 1
-#endif
-constexpr bool kHelperInterleave = CAIRO_HELPER_INTERLEAVE;
 
 struct HelperLds {
   InterLds inter;
@@ -1478,19 +1581,17 @@ struct EngineLds {
 // coder waits for exactly these), and the deblock of row r, chunk by chunk as
 // the coder's granules arrive (advanced whenever the inter search is waiting
 // or done).  Never blocks on its own row coder while an inter group is due.
-// Thread 0's value v, broadcast to the workgroup (two barriers).
-__device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
-  if (threadIdx.x == 0) *slot = v;
-  __syncthreads();
-  const int r = *slot;
-  __syncthreads();
-  return r;
-}
+
+// Row helper (j, r): the inter search of MB row r, group by group as the
+// previous frame becomes final over each group's search window (the row
+// coder waits for exactly these), and the deblock of row r, chunk by chunk as
+// the coder's granules arrive (advanced whenever the inter search is waiting
+// or done).  Never blocks on its own row coder while an inter group is due.
 
 // Helper decision for group g (thread 0): 1 = the inter search may run,
 // 2 = a deblock chunk is ready meanwhile, 0 = nothing yet.
 __device__ __forceinline__ int helper_decision(const FrameArgs& a, int r, int need, const DbState& st, int nch) {
-  const int rr = min(r + 3, a.hmb - 1);
+  const int rr = min(r + 2, a.hmb - 1);  // level 1 of the group's window (inter_task)
   if (!a.prev_deblocked ||
       __hip_atomic_load(a.prev_deblocked + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
     return 1;
@@ -1510,38 +1611,11 @@ __device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds&
   DbState st{0, 0, 0, 8};
   for (int g = 0; g < a.ng; g++) {
     trace(tr, 1, g);
-    const int need = min(64 * g + 96, a.wa);
-    uint64_t t0 = 0;
-    for (;;) {  // until group g may run; deblock meanwhile
-      int d = 0;
-      if (tid == 0) {
-        d = helper_decision(a, r, need, st, nch);
-        if (d == 0) {  // nothing to do: back off, bounded like every wait
-          const uint64_t now = __builtin_amdgcn_s_memrealtime();
-          if (!t0) t0 = now;
-          __builtin_amdgcn_s_sleep(1);
-          if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            d = 1;
-          } else if (now - t0 > 200000000ull) {
-            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            d = 1;
-          }
-        }
-      }
-      d = wg_broadcast(vflag, d);
-      trace(tr, 3, 20 + d);
-      if (d == 1) break;
-      if (d == 2) deblock_chunk(a, r, L.db, st);
-    }
-    if (tid == 0) {  // the readiness check used a relaxed load: acquire what it observed
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
+    // level 1 of the group's window (inter_task); deblock meanwhile
+    helper_wait(a, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     trace(tr, 3, 50);
     if (a.inter) {
-      for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter);
+      for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag);
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
