@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--no-end-to-end", action="store_true")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
     p.add_argument("--batch", type=int, default=16, help="frames per engine launch (pipelined)")
+    p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
     return p.parse_args()
 
 
@@ -137,6 +138,8 @@ def main():
 
     ctx = cairo_amd.Context(w, h, ring, device=local)
     ctx.set_batch(a.batch)
+    if a.rows:
+        ctx.set_workgroups(a.rows)
     stages = ctx.L.cairo_ctx_stages(ctx.h)
 
     def barrier():

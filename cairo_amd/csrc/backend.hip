@@ -37,7 +37,7 @@ constexpr int kStages = 64;      // staging slots (frames in flight): four 16-fr
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
 constexpr int kDefaultBatch = 16;
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
-constexpr int kMaxLaunchWG = 368;  // workgroups per launch: two launches stay co-resident (3 per CU)
+constexpr int kMaxLaunchWG = 384;  // workgroups per launch: two launches fill the 768 slots (3 per CU)
 constexpr int kSuccess = 0, kInvalidArg = 2, kOutOfMemory = 3, kHardwareFail = 5,
               kInvalidResource = 8;
 

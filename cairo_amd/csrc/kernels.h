@@ -86,6 +86,7 @@ struct FrameArgs {
   int32_t* deblocked;  // [hmb] final luma columns per MB row (monotone)
   const int32_t* prev_deblocked;  // the previous frame's, if it is in this batch (else nullptr)
   uint64_t* stamps;    // diagnostic (nullptr = off)
+  uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, 3 stamps (wait, ready, done)
   const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)
 };
 

@@ -1611,8 +1611,11 @@ __device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds&
   DbState st{0, 0, 0, 8};
   for (int g = 0; g < a.ng; g++) {
     trace(tr, 1, g);
+    uint64_t* is = a.istamps && tid == 0 ? a.istamps + (size_t)(r * a.ng + g) * a.nref * 3 : nullptr;
+    if (is) is[0] = __builtin_amdgcn_s_memrealtime();
     // level 1 of the group's window (inter_task); deblock meanwhile
     helper_wait(a, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+    if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
       for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag);
@@ -1621,6 +1624,7 @@ __device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds&
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (is) is[2] = __builtin_amdgcn_s_memrealtime();
     for (;;) {  // catch the deblock up with what has arrived
       int d = 0;
       if (tid == 0) d = kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
@@ -1732,6 +1736,12 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.deblocked = e.sync + SyncLayout::deblocked(e.hmb, a.ng, j);
   a.prev_deblocked = j > 0 ? e.sync + SyncLayout::deblocked(e.hmb, a.ng, j - 1) : e.prev_last_deblocked;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
+  {
+    const int ng = (e.wmb + 3) / 4, nref = e.ring > 1 ? e.ring - 1 : 1;
+    a.istamps = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, e.hmb) + 2 +
+                               (size_t)j * e.hmb * ng * nref * 3
+                         : nullptr;
+  }
   a.rgb = f.rgb;
   return a;
 }

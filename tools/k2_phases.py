@@ -23,6 +23,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="720p")
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--rows", type=int, default=0, help="row-coder workgroups (0 = default)")
+ap.add_argument("--row", type=int, default=10, help="MB row of the group timeline")
+ap.add_argument("--frame", type=int, default=1, help="frame (>= 1) of the batch for the lag / group-timeline sections")
 a = ap.parse_args()
 w, h, ring, q = CFG[a.config]
 ctx = cairo_amd.Context(w, h, ring)
@@ -73,29 +75,31 @@ print(f"  hand-off (publish -> resume) mean {lat.mean():.3f} p50 {np.median(lat)
 clk = (st[..., 11] - st[..., 10]) / np.maximum(st[..., 9] - st[..., 0], 1) * 100.0  # MHz
 print(f"  effective shader clock: mean {clk.mean():.0f} MHz")
 # inter tasks: dequeue -> ready (dependency met) -> done
-ok = ist[..., 2] > 0
+ok = ist[..., 0, 2] > 0
 if ok.any():
-    wait = (ist[..., 1] - ist[..., 0])[ok] / 100.0
-    run = (ist[..., 2] - ist[..., 1])[ok] / 100.0
+    wait = (ist[..., 0, 1] - ist[..., 0, 0])[ok] / 100.0
+    run = (ist[..., 0, 2] - ist[..., 0, 1])[ok] / 100.0
     print(f"inter tasks: {ok.sum()}  wait mean {wait.mean():.1f} us  run mean {run.mean():.1f} us p50 {np.median(run):.1f} "
           f"max {run.max():.1f}")
     for j in range(B):
-        okj = ist[j, ..., 2] > 0
-        if okj.any():
-            print(f"  frame {j}: inter tasks {(ist[j, ..., 0][okj].min() - t0) / 100.0:8.1f} .. "
-                  f"{(ist[j, ..., 2][okj].max() - t0) / 100.0:8.1f} us")
+        okj = ist[j, ..., 0, 2] > 0
+        if okj.any() and j < 4:
+            print(f"  frame {j}: inter tasks {(ist[j, ..., 0, 0][okj].min() - t0) / 100.0:8.1f} .. "
+                  f"{(ist[j, ..., 0, 2][okj].max() - t0) / 100.0:8.1f} us")
 # frame-to-frame lag of MB completion (stamp 9) at sample positions
+F = min(max(a.frame, 1), B - 1)
 if B > 2:
-    print("lag of frame j+1 behind frame j at MB (x, r), us [j=0->1, 1->2, 2->3]:")
+    js = [max(F - 1, 0), F, min(F + 1, B - 2)][: max(1, min(3, B - 1))]
+    print(f"lag of frame j+1 behind frame j at MB (x, r), us [j={js}]:")
     for r in (0, 5, 10, 20, 30, 40, hb - 1):
         row = []
         for x in (0, wb // 2, wb - 1):
-            lags = [(st[j + 1, r, x, 9] - st[j, r, x, 9]) / 100.0 for j in range(3)]
+            lags = [(st[j + 1, r, x, 9] - st[j, r, x, 9]) / 100.0 for j in js]
             row.append(f"x={x:3d}: " + "/".join(f"{v:6.0f}" for v in lags))
         print(f"  r={r:3d}  " + "   ".join(row))
     # how long frame 1's MBs wait at group boundaries (wait phase at bx % 4 == 0)
-    wt = (st[1, :, :, 1] - st[1, :, :, 0]) / 100.0
-    print(f"frame 1 wait phase: at group starts mean {wt[:, 0::4].mean():.1f} us, elsewhere "
+    wt = (st[F, :, :, 1] - st[F, :, :, 0]) / 100.0
+    print(f"frame {F} wait phase: at group starts mean {wt[:, 0::4].mean():.1f} us, elsewhere "
           f"{np.delete(wt, np.s_[0::4], axis=1).mean():.1f} us")
 # deblock chunk k (MB k) publish vs the coding of MB k (stamp 9)
 for j in range(min(B, 2)):
@@ -105,13 +109,13 @@ for j in range(min(B, 2)):
             f"k={k}: {(dbs[j, r, k] - st[j, r, k, 9]) / 100.0:.1f}" for k in ks_))
 # frame 1, row 10: per group, when its inter task became ready / was claimed / done,
 # and when the row coder reached / resumed at the group's first MB
-if B > 1 and hb > 13 and (ist[..., 2] > 0).any():
-    r = 10
-    print(f"frame 1 row {r} per group (us): ready(deblock f0 row {r + 3}) claim done | coder reach resume")
+if B > 1 and hb > 13 and (ist[..., 0, 2] > 0).any():
+    r = a.row if hasattr(a, 'row') else 10
+    print(f"frame {F} row {r} per group (us): ready(deblock f{F - 1} row {r + 2}) wait-start ready done | coder reach resume")
     for g in range(0, (wb + 3) // 4, 3):
-        need = min(64 * g + 96, w)
+        need = min(64 * g + 80, w)  # level 1 of the inter window (kernels.hip inter_need_cols)
         kk = [k for k in range(min(wb, 256)) if (16 * (k + 1) - 12 >= need or k == wb - 1)]
-        ready = (dbs[0, min(r + 3, hb - 1), kk[0]] - t0) / 100.0 if kk else float("nan")
-        c, dn = (ist[1, r, g, 0, 0] - t0) / 100.0, (ist[1, r, g, 0, 2] - t0) / 100.0
-        reach, res = (st[1, r, 4 * g, 0] - t0) / 100.0, (st[1, r, 4 * g, 1] - t0) / 100.0
-        print(f"  g={g:2d}: {ready:8.1f} {c:8.1f} {dn:8.1f} | {reach:8.1f} {res:8.1f}")
+        ready = (dbs[F - 1, min(r + 2, hb - 1), kk[0]] - t0) / 100.0 if kk else float("nan")
+        c, rd, dn = ((ist[F, r, g, 0, k] - t0) / 100.0 for k in range(3))
+        reach, res = (st[F, r, 4 * g, 0] - t0) / 100.0, (st[F, r, 4 * g, 1] - t0) / 100.0
+        print(f"  g={g:2d}: {ready:8.1f} {c:8.1f} {rd:8.1f} {dn:8.1f} | {reach:8.1f} {res:8.1f}")
