@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_set_batch": (I, [P, I]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
+        "cairo_unserialize_slice": (I, [P, ctypes.POINTER(U), U, U, U, U, P, P, P, P]),
         "cairo_stream_create": (I, [P, I, ctypes.POINTER(P)]),
         "cairo_stream_submit": (I, [P, P, I, U, U, U, ctypes.POINTER(I)]),
         "cairo_stream_collect": (I, [P, I, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
@@ -297,6 +298,23 @@ def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv
     )
     n = pos.value
     return out[: (n + 7) // 8].tobytes(), n
+
+
+def unserialize_slice(payload: bytes, nbits: int, wmb: int, hmb: int, ring: int, table=None, planes=None,
+                      start: int = 0):
+    """Host entropy decode of one frame's payload (bits [start, nbits) of
+    payload) into a persistent (table, (y, u, v)) state (zeros when None) ->
+    (table, planes, bits consumed)."""
+    if table is None:
+        table = np.zeros(wmb * hmb, BLOCK_DESC)
+    if planes is None:
+        planes = (np.zeros((hmb * 16, wmb * 16), np.int16), np.zeros((hmb * 8, wmb * 8), np.int16),
+                  np.zeros((hmb * 8, wmb * 8), np.int16))
+    buf = np.frombuffer(payload, np.uint8) if len(payload) else np.zeros(1, np.uint8)
+    rd = ctypes.c_uint32(start)
+    _ck(lib().cairo_unserialize_slice(_ptr(np.ascontiguousarray(buf)), ctypes.byref(rd), nbits, wmb, hmb, ring,
+                                      _ptr(table), *(_ptr(p) for p in planes)), "cairo_unserialize_slice")
+    return table, planes, rd.value - start
 
 
 def bits_append(dst: np.ndarray, pos: int, src: bytes, nbits: int) -> int:

@@ -227,7 +227,7 @@ hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s) {
 // ---------------------------------------------------------------------------
 
 constexpr int kWinL = 80, kWinLW = 128, kWinLP = 136;  // luma rows, width, pitch (elements)
-constexpr int kWinC = 40, kWinCW = 64, kWinCP = 72;    // chroma
+constexpr int kWinC = 40, kWinCP = 72;  // chroma rows, pitch (64 columns)
 
 struct alignas(16) Window {
   int16_t y[kWinL * kWinLP];

@@ -115,6 +115,16 @@ CAIRO_API int cairo_serialize_slice(const uint8_t *block_table, uint32_t wmb, ui
                                     const int16_t *coef_v, uint8_t *out, uint32_t out_bytes,
                                     uint32_t *bit_pos);
 
+/* ---- host entropy decode (unserialize_slice, unserialize.cpp:321-342) ----
+ * Decodes the ABAC payload of one frame starting at bit *read_index of data
+ * (LSB-first, up to write_index) into the block table (wmb*hmb 16-B descs) and
+ * the coefficient planes, which persist across frames: fields a block does not
+ * carry keep their previous values, as in the reference decoder's context.
+ * Advances *read_index.  EVX_ERROR_INVALID_RESOURCE (8) on a corrupt payload. */
+CAIRO_API int cairo_unserialize_slice(const uint8_t *data, uint32_t *read_index, uint32_t write_index,
+                                      uint32_t wmb, uint32_t hmb, uint32_t ring, uint8_t *block_table,
+                                      int16_t *coef_y, int16_t *coef_u, int16_t *coef_v);
+
 /* ---- frame pipeline ---------------------------------
  * GPU hot path + host entropy for a stream of frames: the caller submits
  * frames, a completion thread picks up each frame's outputs, a pool of entropy

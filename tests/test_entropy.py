@@ -79,3 +79,42 @@ def test_bits_append_matches_bitwise_model(cairo):
         assert got == want, (pos, n)
     with pytest.raises(cairo.CairoError):
         cairo.bits_append(np.zeros(2, np.uint8), 10, b"\xff\xff", 7)
+
+
+@pytest.mark.parametrize("ring,q,intra_every", [(4, 16, 4), (2, 1, 0), (3, 31, 0)])
+def test_unserialize_round_trip(orc, cairo, ring, q, intra_every):
+    """Host entropy decode (unserialize.cpp) inverts serialize_slice frame by
+    frame: the persistent coefficient planes equal the encoder's output_cache
+    (copy blocks keep their previous coefficients on both sides) and every
+    block-table field the stream carries for a block is recovered
+    (unserialize.cpp:150-287)."""
+    w, h = 176, 144
+    wmb, hmb = w // 16, h // 16
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    table = planes = None
+    for t in range(6):
+        if intra_every and t % intra_every == 0:
+            e.insert_intra()
+        e.encode(orc.make_frame(w, h, t))
+        et = e.block_table()
+        y, u, v = e.planes(1)
+        pay, nb = cairo.serialize_slice(et, wmb, hmb, ring, y, u, v)
+        table, planes, used = cairo.unserialize_slice(pay, nb, wmb, hmb, ring, table, planes)
+        assert used == nb
+        for a, b, n in zip(planes, (y, u, v), "YUV"):
+            np.testing.assert_array_equal(a, b, err_msg=f"frame {t} coef {n}")
+        bt = et["block_type"]
+        np.testing.assert_array_equal(table["block_type"], bt)
+        inter = (bt & 1) == 0
+        motion = (bt & 2) != 0
+        copy = (bt & 4) != 0
+        # log2((uint8)R) target bits (serialize.cpp:179): R = 3 keeps only bit 0
+        mask = (1 << (int(ring).bit_length() - 1)) - 1
+        np.testing.assert_array_equal(table["prediction_target"][inter], et["prediction_target"][inter] & mask)
+        for f in ("motion_x", "motion_y", "sp_pred"):
+            np.testing.assert_array_equal(table[f][motion], et[f][motion], err_msg=f)
+        sp = motion & (et["sp_pred"] != 0)
+        for f in ("sp_amount", "sp_index"):
+            np.testing.assert_array_equal(table[f][sp], et[f][sp], err_msg=f)
+        np.testing.assert_array_equal(table["q_index"][~copy], et["q_index"][~copy])
