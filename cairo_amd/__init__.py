@@ -100,6 +100,13 @@ def lib() -> ctypes.CDLL:
         "evx_bitstream_data": (P, [P]),
         "evx_bitstream_occupancy": (U, [P]),
         "evx_bitstream_empty": (V, [P]),
+        "evx_bitstream_write_bits": (I, [P, P, U]),
+        "evx_decoder_create": (I, [ctypes.POINTER(P)]),
+        "evx_decoder_destroy": (I, [P]),
+        "evx_decoder_clear": (I, [P]),
+        "evx_decoder_decode": (I, [P, P, P]),
+        "evx_decoder_set_device": (I, [P, I]),
+        "cairo_ctx_decode_frame": (I, [P, P, P, U, P]),
         "cairo_make_band4": (V, [P, U, U, U, U]),
         "cairo_version": (ctypes.c_char_p, []),
         "cairo_device_count": (I, []),
@@ -394,6 +401,12 @@ class BitStream:
     def bits(self) -> int:
         return self.L.evx_bitstream_occupancy(self.h)
 
+    def write(self, data: bytes, nbits: int | None = None) -> None:
+        """Append nbits (default: all) of data, LSB-first."""
+        n = len(data) * 8 if nbits is None else nbits
+        buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+        _ck(self.L.evx_bitstream_write_bits(self.h, _ptr(np.ascontiguousarray(buf)), n), "write_bits")
+
     def data(self) -> bytes:
         n = (self.bits() + 7) // 8
         return ctypes.string_at(self.L.evx_bitstream_data(self.h), n) if n else b""
@@ -446,6 +459,54 @@ class Encoder:
             self.close()
         except Exception:
             pass
+
+
+class Decoder:
+    """The drop-in evx1_decoder (reference evx1.h:97-112) through its C view."""
+
+    def __init__(self, device: int = 0):
+        self.L = lib()
+        p = ctypes.c_void_p()
+        _ck(self.L.evx_decoder_create(ctypes.byref(p)), "create_decoder")
+        self.h = p
+        if device:
+            _ck(self.L.evx_decoder_set_device(self.h, device), "set_device")
+
+    def decode(self, bs: "BitStream", width: int, height: int) -> np.ndarray:
+        """Decode [header +] one frame record of bs (emptied afterwards) -> RGB (h, w, 3)."""
+        out = np.zeros((height, width, 3), np.uint8)
+        _ck(self.L.evx_decoder_decode(self.h, bs.h, _ptr(out)), "decode")
+        return out
+
+    def clear(self) -> None:
+        _ck(self.L.evx_decoder_clear(self.h), "clear")
+
+    def close(self) -> None:
+        if self.h:
+            self.L.evx_decoder_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def yuv_to_rgb(y: np.ndarray, u: np.ndarray, v: np.ndarray, width: int, height: int) -> np.ndarray:
+    """convert_image YUV -> RGB (reference convert.cpp:16-19, 162-223), numpy
+    restatement for tests: saturate narrows to int16, then clips to 0..255."""
+    yy = y[:height, :width].astype(np.int32) - 16
+    uu = np.repeat(np.repeat(u.astype(np.int32) - 128, 2, 0), 2, 1)[:height, :width]
+    vv = np.repeat(np.repeat(v.astype(np.int32) - 128, 2, 0), 2, 1)[:height, :width]
+
+    def sat(x):
+        x = ((x + 32768) & 0xFFFF) - 32768
+        return np.clip(x, 0, 255).astype(np.uint8)
+
+    return np.stack([sat((256 * yy + 358 * vv + 128) >> 8),
+                     sat((256 * yy - 88 * uu - 182 * vv + 128) >> 8),
+                     sat((256 * yy + 452 * uu + 128) >> 8)], axis=-1)
 
 
 def device_count() -> int:

@@ -38,7 +38,7 @@ constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engi
 constexpr int kDefaultBatch = 16;
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 constexpr int kMaxLaunchWG = 384;  // workgroups per launch: two launches fill the 768 slots (3 per CU)
-constexpr int kSuccess = 0, kInvalidArg = 2, kOutOfMemory = 3, kHardwareFail = 5,
+constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)
               kInvalidResource = 8;
 
 struct Stage {
@@ -230,6 +230,7 @@ int flush(cairo_ctx* c) {
   bool any_inter = false;
   for (int i = 0; i < c->npend; i++) any_inter |= c->pend[i].inter && c->ring > 1;
   e.fa = fd;
+  e.decode = c->pend[0].decode;  // a launch never mixes (decode_frame flushes first)
   const int rows = e.nframes * e.hmb;
   const int ng = (e.wmb + 3) / 4;
   (void)any_inter;
@@ -265,10 +266,17 @@ int flush(cairo_ctx* c) {
     int r = collect_times(c, *tb);  // its events are about to be reused
     if (r) return r;
   }
-  for (int i = 0; i < e.nframes; i++)  // host RGB sources
-    if (c->pend[i].host_rgb)
-      CK(hipMemcpyAsync((void*)c->pend[i].rgb, c->pend[i].host_rgb, (size_t)c->w * c->h * 3,
+  for (int i = 0; i < e.nframes; i++) {  // host RGB sources; the decoder's table and coefficients
+    const FrameDesc& f = c->pend[i];
+    if (f.host_rgb)
+      CK(hipMemcpyAsync((void*)f.rgb, f.host_rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, st));
+    if (f.decode) {
+      CK(hipMemcpyAsync(c->table + (size_t)f.slot * c->mbs, f.host_table, c->mbs * sizeof(BlockDesc),
                         hipMemcpyHostToDevice, st));
+      CK(hipMemcpyAsync(c->coef + (size_t)f.slot * c->plane_elems, f.host_coef, c->plane_elems * 2,
+                        hipMemcpyHostToDevice, st));
+    }
+  }
   CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(e.sync, 0, c->sync_words * sizeof(int32_t), st));
   CK(hipEventRecord(c->area_ready[area], st));
@@ -295,6 +303,10 @@ int flush(cairo_ctx* c) {
   for (int i = 0; i < e.nframes; i++) {
     const int slot = c->pend[i].slot;
     Stage& s = c->st[slot];
+    if (c->pend[i].decode) {  // the decoder's output is the slot (decode_frame converts it)
+      s.launched = true;
+      continue;
+    }
     CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
                       hipMemcpyDeviceToHost, c->cs));
     CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2,
@@ -495,6 +507,9 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   f.epoch = ++c->epoch;
   f.slot = slot;
   f.prev_slot = (t + kStages - 1) % kStages;
+  f.decode = 0;  // decode_frame never leaves a decode frame pending
+  f.host_table = nullptr;
+  f.host_coef = nullptr;
   c->npend++;
   s.busy = true;
   s.launched = false;
@@ -556,6 +571,59 @@ int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
     }
   }
   return frame_result(c, s, out);
+}
+
+int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* coef, uint32_t index,
+                           uint8_t* rgb) {
+  if (!c || !table || !coef || !rgb) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  CK(hipSetDevice(c->device));
+  int r = flush(c);  // encode frames still pending go first, in their own launch
+  if (r) return r;
+  const int t = c->next_ticket, slot = t % kStages;
+  Stage& s = c->st[slot];
+  if (s.busy) {
+    fprintf(stderr, "[cairo_amd] staging slot of ticket %d not released\n", s.ticket);
+    return kInvalidResource;
+  }
+  FrameDesc& f = c->pend[0];
+  memset(&f, 0, sizeof(f));
+  f.index = (int)index;
+  f.inter = 1;
+  f.quality = 1;
+  f.epoch = ++c->epoch;
+  f.slot = slot;
+  f.prev_slot = (t + kStages - 1) % kStages;
+  f.decode = 1;
+  f.host_table = reinterpret_cast<const BlockDesc*>(table);
+  f.host_coef = coef;
+  c->npend = 1;
+  s.busy = true;
+  s.launched = false;
+  s.ticket = t;
+  s.index = index;
+  s.type = 1;
+  s.quality = 0;
+  c->next_ticket++;
+  const long long b = c->batches;  // the launch flush() is about to make
+  r = flush(c);
+  if (r == kSuccess) {
+    hipStream_t st = (b & 1) ? c->ks2 : c->ks;
+    uint8_t* drgb = c->rgb + (size_t)slot * c->w * c->h * 3;
+    r = fail(launch_yuv_to_rgb(slot_planes(c->ring_buf, c, (int)(index % c->ring)), (int)c->wa, (int)c->w,
+                               (int)c->h, drgb, st), "launch_yuv_to_rgb");
+    if (r == kSuccess)
+      r = fail(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    if (r == kSuccess)
+      r = fail(hipMemcpyAsync(rgb, drgb, (size_t)c->w * c->h * 3, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    if (r == kSuccess) r = fail(hipStreamSynchronize(st), "hipStreamSynchronize");
+    if (r == kSuccess && *s.err) {
+      fprintf(stderr, "[cairo_amd] an in-kernel wait timed out (decoding frame %u)\n", index);
+      r = kHardwareFail;
+    }
+  }
+  s.busy = false;
+  return r;
 }
 
 int cairo_ctx_release(cairo_ctx* c, int ticket) {

@@ -176,4 +176,7 @@ void evx_bitstream_destroy(void *bs) { delete (evx::bit_stream *)bs; }
 const uint8_t *evx_bitstream_data(void *bs) { return ((evx::bit_stream *)bs)->query_data(); }
 uint32_t evx_bitstream_occupancy(void *bs) { return ((evx::bit_stream *)bs)->query_occupancy(); }
 void evx_bitstream_empty(void *bs) { ((evx::bit_stream *)bs)->empty(); }
+int evx_bitstream_write_bits(void *bs, const void *data, uint32_t count) {
+  return ((evx::bit_stream *)bs)->write_bits(const_cast<void *>(data), count);
+}
 }

@@ -14,6 +14,7 @@
 #include "../../include/evx1.h"
 #include "entropy.h"
 #include "evx_defs.h"
+#include "stream_format.h"
 
 namespace evx {
 
@@ -22,25 +23,6 @@ namespace {
 constexpr uint32 kDefaultRing = 4;         // EVX_REFERENCE_FRAME_COUNT, config.h:39
 constexpr uint16 kDefaultQuality = 8;      // EVX_DEFAULT_QUALITY_LEVEL, config.h:40
 constexpr uint32 kPeriodicIntra = 3600;    // EVX_PERIODIC_INTRA_RATE, config.h:41
-constexpr uint16 kVersionWord = (2 << 8) | 47;  // EVX_VERSION_WORD(2, 47), version.h:37-41
-
-#pragma pack(push, 2)
-struct header_t {  // evx_header, common.h:50-62
-  uint8 magic[4];
-  uint16 size;
-  uint8 ref_count;
-  uint16 version;
-  uint16 frame_width;
-  uint16 frame_height;
-};
-struct frame_t {  // evx_frame, common.h:66-72
-  uint32 type;
-  uint32 index;
-  uint16 quality;
-};
-#pragma pack(pop)
-static_assert(sizeof(header_t) == 14, "evx_header is 14 bytes");
-static_assert(sizeof(frame_t) == 10, "evx_frame is 10 bytes");
 
 int clip_quality(int q) { return q < 1 ? 1 : (q > 31 ? 31 : q); }
 

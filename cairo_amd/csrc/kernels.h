@@ -57,6 +57,9 @@ struct FrameDesc {
   uint32_t epoch;      // granule tag (per-context submission count, never 0)
   int slot;            // staging slot: this frame's source / coefficient / table / granule buffers
   int prev_slot;       // staging slot of the previous frame (output_cache chain)
+  int decode;          // 1: reconstruct from the slot's table + coefficients (the decoder), no search
+  const BlockDesc* host_table;  // decode: the frame's block table and coefficient planes (y, u, v
+  const int16_t* host_coef;     //   contiguous), uploaded at launch
 };
 
 // Per-frame view of the engine's state, built by the host for every frame of
@@ -68,6 +71,7 @@ struct FrameArgs {
   int wmb, hmb;        // macroblocks per row / column
   int ring;            // R = ring size (EVX_REFERENCE_FRAME_COUNT)
   int index, inter, quality;
+  int decode;          // decode mode (FrameDesc::decode): table and coef are inputs
   uint32_t epoch;
   PlaneSet in;         // input_cache of this frame
   PlaneSet coef;       // output_cache of this frame (persistent semantics: copy MBs carry coef_prev)
@@ -134,6 +138,7 @@ struct EngineArgs {
   int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)
   const int32_t* order;    // [nframes * hmb] task order of every pool: (frame << 16 | row),
                            // sorted by (row + kOrderSlope * frame, frame)
+  int decode;              // the launch decodes (every frame has FrameDesc::decode set)
 };
 
 // Frame-row task order of the engine pools.  A task of frame f, row r waits
@@ -150,6 +155,10 @@ hipError_t launch_engine(const EngineArgs& e, hipStream_t s);
 // Debug: rebuild the pre-deblock reconstruction of frame j of the batch from
 // its granules into plane set dst.
 hipError_t launch_unpack_granules(const EngineArgs& e, int j, PlaneSet dst, hipStream_t s);
+
+// convert_image YUV -> RGB (convert.cpp:16-19, 162-223) of plane set src into
+// RGB888 rgb (w x h, pitch 3*w).
+hipError_t launch_yuv_to_rgb(PlaneSet src, int wa, int w, int h, uint8_t* rgb, hipStream_t s);
 
 // Known-answer entry points: apply the device transform / quantizer code to
 // a batch of macroblocks (6 blocks of 64 int16 each, block-major).

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_convert_batch(EngineArgs e) {
   const FrameArgs& f = e.fa[blockIdx.z];
   const int qx = blockIdx.x * 256 + threadIdx.x;  // quad column
   const int qy = blockIdx.y;                      // quad row
-  if (qx >= (e.w >> 1)) return;
+  if (qx >= (e.w >> 1) || f.decode) return;
   const PlaneSet in = f.in;
   int su = 0, sv = 0;
 #pragma unroll
@@ -1275,6 +1275,9 @@ __device__ __forceinline__ void coef_store_pair(const FrameArgs& a, int e, int p
 
 // Code MB row `by` of frame a (intra search, classify, transform, VAQ,
 // quantize, reconstruct), left to right; whole workgroup.
+// kDecode: the decoder's reconstruction (decode_slice, decode.cpp:146-170) from
+// the given block table and coefficients, without the searches.
+template <bool kDecode>
 __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, int32_t* tr) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
@@ -1320,8 +1323,8 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
         }
       }
       // source rows of this lane's group slot
-      SrcRow s;  // biased u16 pairs
-      {
+      SrcRow s;  // biased u16 pairs (the encoder's source; unused when decoding)
+      if (!kDecode) {
         const uint4* ry = (const uint4*)(a.in.y + (size_t)(py + gi) * a.wa + px);
         const uint4 r0 = ry[0], r1 = ry[1];
         s.y[0] = r0.x, s.y[1] = r0.y, s.y[2] = r0.z, s.y[3] = r0.w;
@@ -1368,80 +1371,99 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
       __syncthreads();
       stamp(a, mb, 2);
 
-      // ---- intra search (calculate_intra_prediction, motion.cpp:354-419) ----
-      Sel sel;
-      {
-        int sm = 0;
-#pragma unroll
-        for (int k = 0; k < 16; k++) sm += abs(src_px(s.y, k));
-        sel.sad = uni(row16_sum(sm));  // compute_block_sad(src): every group holds the total
-      }
-      sel.bx = px;
-      sel.by = py;
-      sel.mad = INT32_MAX;
-      sel.ssd = INT32_MAX;
-      sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
-      int buf = 0;
-#pragma unroll 1
-      for (int stage = 0; stage < 5; stage++) {
-        const int step = stage == 0 ? kRadius : (kRadius >> stage);
-        const int jlo = stage == 0 ? -2 * kRadius : -step;
-        const int bx0 = sel.bx, by0 = sel.by;
-        {  // group g < 9 evaluates candidate g; groups 9..15 repeat candidate 8
-          const int c = min(grp, 8);
-          const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
-          const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
+      BlockDesc d;
+      bool from_inter = false;  // an inter record won / an inter type is decoded (prediction in wpv)
+      int wpv[2] = {0, 0};
+      if (!kDecode) {
+        // ---- intra search (calculate_intra_prediction, motion.cpp:354-419) ----
+        Sel sel;
+        {
+          int sm = 0;
+  #pragma unroll
+          for (int k = 0; k < 16; k++) sm += abs(src_px(s.y, k));
+          sel.sad = uni(row16_sum(sm));  // compute_block_sad(src): every group holds the total
+        }
+        sel.bx = px;
+        sel.by = py;
+        sel.mad = INT32_MAX;
+        sel.ssd = INT32_MAX;
+        sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
+        int buf = 0;
+  #pragma unroll 1
+        for (int stage = 0; stage < 5; stage++) {
+          const int step = stage == 0 ? kRadius : (kRadius >> stage);
+          const int jlo = stage == 0 ? -2 * kRadius : -step;
+          const int bx0 = sel.bx, by0 = sel.by;
+          {  // group g < 9 evaluates candidate g; groups 9..15 repeat candidate 8
+            const int c = min(grp, 8);
+            const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
+            const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
+            int sad, mad;
+            cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
+            if (gi == 0 && grp < 9) {
+              L.cand[buf][grp][0] = ok ? sad : -1;
+              L.cand[buf][grp][1] = mad;
+            }
+          }
+          __syncthreads();
+          {
+            const int c = lane & 15;
+            const int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
+            const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
+            select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
+          }
+          buf ^= 1;
+        }
+        stamp(a, mb, 3);
+        {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
+          const int bx0 = sel.bx, by0 = sel.by;
+          const int nn = grp >> 1, q = grp & 1;
+          const int k9 = nn < 4 ? nn : nn + 1;  // skip the centre of the 3x3
+          const int tx = bx0 + k9 % 3 - 1, ty = by0 + k9 / 3 - 1;
+          const bool ok = intra_valid(tx, ty, px, py, a.wa, a.ha);
           int sad, mad;
-          cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
-          if (gi == 0 && grp < 9) {
+          subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, q, gi, s, sad, mad);
+          if (gi == 0) {
             L.cand[buf][grp][0] = ok ? sad : -1;
             L.cand[buf][grp][1] = mad;
           }
+          __syncthreads();
+          const int vs = L.cand[buf][lane & 15][0], vm = L.cand[buf][lane & 15][1];
+          sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
+          select_sub(sel, vs >= 0, vs, vm, thr, lane);
         }
-        __syncthreads();
-        {
-          const int c = lane & 15;
-          const int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
-          const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
-          select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
-        }
-        buf ^= 1;
-      }
-      stamp(a, mb, 3);
-      {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
-        const int bx0 = sel.bx, by0 = sel.by;
-        const int nn = grp >> 1, q = grp & 1;
-        const int k9 = nn < 4 ? nn : nn + 1;  // skip the centre of the 3x3
-        const int tx = bx0 + k9 % 3 - 1, ty = by0 + k9 / 3 - 1;
-        const bool ok = intra_valid(tx, ty, px, py, a.wa, a.ha);
-        int sad, mad;
-        subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, q, gi, s, sad, mad);
-        if (gi == 0) {
-          L.cand[buf][grp][0] = ok ? sad : -1;
-          L.cand[buf][grp][1] = mad;
-        }
-        __syncthreads();
-        const int vs = L.cand[buf][lane & 15][0], vm = L.cand[buf][lane & 15][1];
-        sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
-        select_sub(sel, vs >= 0, vs, vm, thr, lane);
-      }
-      stamp(a, mb, 4);
-      BlockDesc d = make_desc(sel, px, py, thr, true, 0);
-      int best_sad = sel.sad;
-      bool from_inter = false;  // an inter record won (its prediction is in wpv)
-      int wpv[2] = {0, 0};
+        stamp(a, mb, 4);
+        d = make_desc(sel, px, py, thr, true, 0);
+        int best_sad = sel.sad;
 
-      // ---- classify_block (encode.cpp:17-67) ----
-#pragma unroll
-      for (int o = 0; o < kMaxRing - 1; o++) {
-        if (o >= nref) break;
-        const bool ci = (inter_d[o].block_type & kCopy) != 0, cb = (d.block_type & kCopy) != 0;
-        if (ci != cb ? ci : inter_sad[o] < best_sad) {
-          d = inter_d[o];
-          best_sad = inter_sad[o];
+        // ---- classify_block (encode.cpp:17-67) ----
+  #pragma unroll
+        for (int o = 0; o < kMaxRing - 1; o++) {
+          if (o >= nref) break;
+          const bool ci = (inter_d[o].block_type & kCopy) != 0, cb = (d.block_type & kCopy) != 0;
+          if (ci != cb ? ci : inter_sad[o] < best_sad) {
+            d = inter_d[o];
+            best_sad = inter_sad[o];
+            from_inter = true;
+            wpv[0] = ipv[o][0];
+            wpv[1] = ipv[o][1];
+          }
+        }
+      } else {
+        // ---- decoder (decode_slice, decode.cpp:146-170): the block desc is
+        //      given; an inter type predicts from its reference slot ----
+        d = uni_desc(a.table[mb]);
+        d.q_index = (uint8_t)uni(a.table[mb].q_index);  // uni_desc leaves it to the quantizer
+        if (!(d.block_type & kIntra)) {
           from_inter = true;
-          wpv[0] = ipv[o][0];
-          wpv[1] = ipv[o][1];
+          const PlaneSet rp = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
+                                        (int)(((uint32_t)a.index + a.ring - d.prediction_target) % a.ring));
+          const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
+          int dx = 0, dy = 0;
+          if (sp) frac_dir(d.sp_index, &dx, &dy);
+          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
+            wpv[bi] = pred_global(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
+                                  py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
         }
       }
       stamp(a, mb, 5);
@@ -1473,7 +1495,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
           pv[bi] = v;
         }
       }
-      if (!(type & kCopy)) {
+      if (!(type & kCopy) && !kDecode) {
         _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {  // residual (int16) -> forward transform
           const int b = wave + 4 * bi, e = b * 64 + lane;
           int pl, ex, ey;
@@ -1485,14 +1507,26 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
       }
       stamp(a, mb, 6);
       if (!(type & kCopy)) {
-        int32_t v2;
-        const int qp = vaq_mb(L.red, wave, lane, cf[0], a.quality, &v2);
-        d.q_index = (uint8_t)qp;
-        d.variance = (int16_t)v2;
+        int qp;
+        if (!kDecode) {
+          int32_t v2;
+          qp = vaq_mb(L.red, wave, lane, cf[0], a.quality, &v2);
+          d.q_index = (uint8_t)qp;
+          d.variance = (int16_t)v2;
+        } else {
+          qp = d.q_index;
+        }
         _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
           const int b = wave + 4 * bi, e = b * 64 + lane;
-          const int16_t qv = quant_elem(e, cf[bi], qp, intra_path);
-          coef_store_pair(a, e, px, py, qv);
+          int16_t qv;
+          if (!kDecode) {
+            qv = quant_elem(e, cf[bi], qp, intra_path);
+            coef_store_pair(a, e, px, py, qv);
+          } else {  // the decoded coefficients (the decoder's input_cache)
+            int pl, ex, ey;
+            elem_coords(e, px, py, pl, ex, ey);
+            qv = plane_of(a.coef, pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+          }
           const int t = idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
                                   dequant_elem(e, qv, qp, intra_path));
           pv[bi] = (int16_t)(has_pred ? t + pv[bi] : t);  // reconstruction (unclamped)
@@ -1500,7 +1534,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
       } else {  // copy: output_cache keeps this macroblock's previous coefficients
         d.q_index = 0;
         d.variance = 0;
-        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+        if (!kDecode) _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
           const int e = (wave + 4 * bi) * 64 + lane;
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
@@ -1543,7 +1577,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
                     gran_settle(gran_at(a, bx + 3, by - 2, tid), pg2, tag, err, a.sticky));
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
-      if (tid == 0) a.table[mb] = d;
+      if (tid == 0 && !kDecode) a.table[mb] = d;
       // every wave's coefficient stores drained, then the block info for the
       // deblock (its edge strengths); thread 0's drain covers only wave 0, so
       // the other waves drain before the barrier of the next macroblock --
@@ -1660,6 +1694,7 @@ __device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds&
 // deadlock with every workgroup resident.
 // ---------------------------------------------------------------------------
 
+template <bool kDecode>
 __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   __shared__ EngineLds L;
   const int b = blockIdx.x, hmb = e.hmb;
@@ -1682,7 +1717,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
       trace(e.trace, 0, 3000000 + t);
       if (t >= total) break;
       const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
-      code_row(e.fa[j], r, L.u.row, e.trace);
+      code_row<kDecode>(e.fa[j], r, L.u.row, e.trace);
       trace(e.trace, 0, 4000000 + t);
     }
   }
@@ -1715,7 +1750,8 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   FrameArgs a{};
   a.wa = e.wa, a.ha = e.ha, a.w = e.w, a.h = e.h, a.wmb = e.wmb, a.hmb = e.hmb, a.ring = e.ring;
   a.index = f.index;
-  a.inter = f.inter && e.ring > 1;
+  a.decode = f.decode;
+  a.inter = f.inter && e.ring > 1 && !f.decode;  // a decoded frame's helpers only carry dependencies
   a.quality = f.quality;
   a.epoch = f.epoch;
   a.in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
@@ -1747,10 +1783,44 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
 }
 
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s) {
-  hipLaunchKernelGGL(k_engine, dim3(e.n_helpers + e.n_rows), dim3(256), 0, s, e);
+  if (e.decode)
+    hipLaunchKernelGGL(k_engine<true>, dim3(e.n_helpers + e.n_rows), dim3(256), 0, s, e);
+  else
+    hipLaunchKernelGGL(k_engine<false>, dim3(e.n_helpers + e.n_rows), dim3(256), 0, s, e);
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// convert_image YUV -> RGB (convert.cpp:16-19, 75-93, 162-223): one thread per
+// horizontal pixel pair; saturate narrows to int16 before clipping
+// (math.h:218-221).  The crop is min(W, Wa) x min(H, Ha) = W x H.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint8_t sat8(int32_t v) {
+  const int16_t s = (int16_t)v;
+  return (uint8_t)(s < 0 ? 0 : (s > 255 ? 255 : s));
+}
+
+__global__ __launch_bounds__(256) void k_yuv_to_rgb(PlaneSet src, int wa, int w, int h, uint8_t* rgb) {
+  const int x2 = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+  if (2 * x2 >= w) return;
+  const int u = src.u[(size_t)(y >> 1) * (wa >> 1) + x2] - 128;
+  const int v = src.v[(size_t)(y >> 1) * (wa >> 1) + x2] - 128;
+  uint8_t* o = rgb + ((size_t)y * w + 2 * x2) * 3;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int yy = src.y[(size_t)y * wa + 2 * x2 + k] - 16;
+    o[3 * k] = sat8((256 * yy + 358 * v + 128) >> 8);
+    o[3 * k + 1] = sat8((256 * yy - 88 * u - 182 * v + 128) >> 8);
+    o[3 * k + 2] = sat8((256 * yy + 452 * u + 128) >> 8);
+  }
+}
+
+hipError_t launch_yuv_to_rgb(PlaneSet src, int wa, int w, int h, uint8_t* rgb, hipStream_t s) {
+  hipLaunchKernelGGL(k_yuv_to_rgb, dim3((w / 2 + 255) / 256, h), dim3(256), 0, s, src, wa, w, h, rgb);
+  return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------
 // KAT: transform/quantize/reconstruct chain on independent macroblocks.

@@ -38,7 +38,7 @@
 
 namespace {
 
-constexpr int kSuccess = 0, kInvalidArg = 2, kCapacityLimit = 7, kInvalidResource = 8;
+constexpr int kSuccess = 0, kInvalidArg = 1, kCapacityLimit = 7, kInvalidResource = 8;  // evx_status (base.h:150-172)
 
 double now_us() {
   return std::chrono::duration<double, std::micro>(

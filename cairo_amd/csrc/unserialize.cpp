@@ -285,7 +285,7 @@ extern "C" int cairo_unserialize_slice(const uint8_t* data, uint32_t* read_index
                                        uint32_t wmb, uint32_t hmb, uint32_t ring, uint8_t* block_table,
                                        int16_t* coef_y, int16_t* coef_u, int16_t* coef_v) {
   if (!data || !read_index || !block_table || !coef_y || !coef_u || !coef_v || *read_index > write_index)
-    return 2;
+    return 1;  // EVX_ERROR_INVALIDARG
   return cairo::unserialize_slice(data, read_index, write_index, wmb, hmb, ring,
                                   reinterpret_cast<cairo::BlockDesc*>(block_table), coef_y, coef_u, coef_v);
 }

@@ -61,6 +61,8 @@ class bit_stream {
    * the tail so the entropy stage can append without per-bit calls. */
   uint32 query_write_index() const { return write_index; }
   void advance_write_index(uint32 bits) { write_index += bits; }
+  uint32 query_read_index() const { return read_index; }
+  void set_read_index(uint32 bits) { read_index = bits; }
 
  private:
   bit_stream(const bit_stream &);

@@ -64,6 +64,14 @@ CAIRO_API int cairo_ctx_submit(cairo_ctx *ctx, const uint8_t *rgb, int rgb_on_de
                                uint32_t index, uint32_t type, uint32_t quality, int *ticket);
 /* Wait until the frame's block table and coefficients are host-visible. */
 CAIRO_API int cairo_ctx_wait(cairo_ctx *ctx, int ticket, cairo_frame_result *out);
+/* The decoder's hot path (decode_slice + deblock + convert_image,
+ * decode.cpp:146-198): reconstruct frame `index` from its block table
+ * (wmb*hmb 16-B descs) and coefficient planes (y | u | v contiguous, the
+ * decoder's input_cache) into ring slot index % R, deblock it, and write it as
+ * RGB888 (width*height*3, pitch 3*width) to host memory rgb.  Synchronous.
+ * The descs must be valid (motion inside the frame; see decoder.cpp). */
+CAIRO_API int cairo_ctx_decode_frame(cairo_ctx *ctx, const uint8_t *block_table, const int16_t *coef,
+                                     uint32_t index, uint8_t *rgb);
 /* Hand the ticket's staging buffers back (required before ticket+stages). */
 CAIRO_API int cairo_ctx_release(cairo_ctx *ctx, int ticket);
 /* Launch any pending frames and block until all GPU work is finished. */
@@ -169,12 +177,24 @@ CAIRO_API int evx_encoder_encode(void *enc, const void *rgb, uint32_t width, uin
 CAIRO_API int evx_encoder_set_ring(void *enc, uint32_t ring); /* before first encode */
 CAIRO_API int evx_encoder_set_device(void *enc, int device);  /* before first encode */
 
+/* ---- drop-in decoder, C view of evx1_decoder (evx1.h:97-112) ------------
+ * decode() reads [header +] one frame record from bs (its read index onward),
+ * writes the frame as RGB888 (width*height*3 from the stream header) to rgb,
+ * and empties bs, as the reference does (evx1dec.cpp:90-124). */
+CAIRO_API int evx_decoder_create(void **dec);
+CAIRO_API int evx_decoder_destroy(void *dec);
+CAIRO_API int evx_decoder_clear(void *dec);
+CAIRO_API int evx_decoder_decode(void *dec, void *bs, void *rgb);
+CAIRO_API int evx_decoder_set_device(void *dec, int device); /* before first decode */
+
 /* bit_stream (reference bitstream.h:43-92) */
 CAIRO_API void *evx_bitstream_create(uint32_t size_in_bits);
 CAIRO_API void evx_bitstream_destroy(void *bs);
 CAIRO_API const uint8_t *evx_bitstream_data(void *bs);
 CAIRO_API uint32_t evx_bitstream_occupancy(void *bs); /* bits */
 CAIRO_API void evx_bitstream_empty(void *bs);
+/* Append count bits of data (LSB-first) -- bit_stream::write_bits. */
+CAIRO_API int evx_bitstream_write_bits(void *bs, const void *data, uint32_t count);
 
 /* band4 synthetic content generator; RGB888, pitch 3*w. */
 CAIRO_API void cairo_make_band4(uint8_t *rgb, uint32_t w, uint32_t h, uint32_t t, uint32_t seed);

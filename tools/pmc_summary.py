@@ -31,7 +31,7 @@ def per_kernel(path):
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
         for k, short in SHORT.items():
-            if f"::{k}(" in name:
+            if f"::{k}(" in name or f"::{k}<false>(" in name:
                 vals.setdefault(short, []).append(float(r["Counter_Value"]))
     # drop the first dispatch of each kernel (warm-up: intra frame, cold caches)
     return {k: v[1:] if len(v) > 1 else v for k, v in vals.items()}
