@@ -598,34 +598,47 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
         }
       }
       if (!need) continue;
+      // The 9 (or 16) candidates of a step are independent: evaluate them all
+      // first (their wave reductions overlap), then replay the sequential
+      // acceptance in scan order (j-outer, i-inner, motion.cpp:225-275) on
+      // the wave-uniform results.  An out-of-frame candidate is evaluated at
+      // the current best and not offered.
       if (si < 5) {
         const int bx = s.bx, by = s.by;
-        for (int j = -step; j <= step; j += step)
-          for (int i = -step; i <= step; i += step) {
-            const int cx = bx + i, cy = by + j;
-            if (!in_frame(cx, cy, a.wa, a.ha)) continue;
-            int sad, mad;
-            sad_mad(src, px_from_window(L.win, cx - ox, cy - oy), sad, mad);
-            accept_int(s, cx, cy, sad, mad, px, py, thr);
-          }
+        int cs[9], cm[9];
+#pragma unroll
+        for (int c = 0; c < 9; c++) {
+          const int cx = bx + (c % 3 - 1) * step, cy = by + (c / 3 - 1) * step;
+          const bool ok = in_frame(cx, cy, a.wa, a.ha);
+          sad_mad(src, px_from_window(L.win, (ok ? cx : bx) - ox, (ok ? cy : by) - oy), cs[c], cm[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 9; c++) {
+          const int cx = bx + (c % 3 - 1) * step, cy = by + (c / 3 - 1) * step;
+          if (in_frame(cx, cy, a.wa, a.ha)) accept_int(s, cx, cy, cs[c], cm[c], px, py, thr);
+        }
       } else {
         // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
         const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
         s.sp_idx = s.sp_amt = s.sp_en = 0;
         const int bx = s.bx, by = s.by;
-        for (int j = -1; j <= 1; j++)
-          for (int i = -1; i <= 1; i++) {
-            if (i == 0 && j == 0) continue;
-            const int tx = bx + i, ty = by + j;
-            if (!in_frame(tx, ty, a.wa, a.ha)) continue;
-            const Px6 nb = px_from_window(L.win, tx - ox, ty - oy);
-            const int idx = frac_index(i, j);
-            for (int q = 0; q < 2; q++) {
-              int sad, mad;
-              sad_mad(src, lerp6(best, nb, q), sad, mad);
-              accept_sub(s, idx, q, sad, mad, thr);
-            }
-          }
+        int cs[16], cm[16];
+#pragma unroll
+        for (int n = 0; n < 8; n++) {
+          const int k9 = n < 4 ? n : n + 1, tx = bx + k9 % 3 - 1, ty = by + k9 / 3 - 1;
+          const bool ok = in_frame(tx, ty, a.wa, a.ha);
+          const Px6 nb = px_from_window(L.win, (ok ? tx : bx) - ox, (ok ? ty : by) - oy);
+#pragma unroll
+          for (int q = 0; q < 2; q++) sad_mad(src, lerp6(best, nb, q), cs[2 * n + q], cm[2 * n + q]);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; n++) {
+          const int k9 = n < 4 ? n : n + 1, i = k9 % 3 - 1, j = k9 / 3 - 1;
+          if (!in_frame(bx + i, by + j, a.wa, a.ha)) continue;
+          const int idx = frac_index(i, j);
+#pragma unroll
+          for (int q = 0; q < 2; q++) accept_sub(s, idx, q, cs[2 * n + q], cm[2 * n + q], thr);
+        }
       }
     }
   }
