@@ -109,13 +109,14 @@ def _table_equal(a, b, what):
         assert bad.size == 0, f"{what}: field {f} differs at MBs {bad[:10]} gpu={a[f][bad[:5]]} ref={b[f][bad[:5]]}"
 
 
-def _run_frames(orc, cairo, w, h, ring, q, frames, intra_only=False, check_inter=True):
+def _run_frames(orc, cairo, w, h, ring, q, frames, intra_only=False, check_inter=True, gen=None):
+    gen = gen or orc.make_frame
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
     ctx = cairo.Context(w, h, ring)
     ctx.set_debug(1)
     for t in range(frames):
-        rgb = orc.make_frame(w, h, t)
+        rgb = gen(w, h, t)
         inter = t > 0 and not intra_only
         if intra_only:
             e.insert_intra()
@@ -173,6 +174,29 @@ def test_frames_1080p_padding(orc, cairo):
     _run_frames(orc, cairo, 1920, 1080, 4, 8, 2)  # Ha = 1088: 8 zero rows
 
 
+def test_frames_4k(orc, cairo):
+    """BASELINE.json configs[3] geometry (the largest frame): I + P, R = 4,
+    every intermediate bit-exact."""
+    _run_frames(orc, cairo, 3840, 2160, 4, 16, 2)
+
+
+# Content beyond band4 (tests/content.py): noise, static, flat extremes,
+# near-ties, out-of-range motion with a scene cut, sub-pel gradients.
+@pytest.mark.parametrize("kind,q", [("noise", 16), ("static", 16), ("black", 8), ("white", 31), ("ties", 1), ("ties", 16),
+                                    ("pan", 16), ("gradient", 1), ("gradient", 16)])
+def test_frames_content(orc, cairo, kind, q):
+    from tests import content
+
+    _run_frames(orc, cairo, 352, 288, 4, q, 5, gen=lambda w, h, t: content.make(kind, w, h, t))
+
+
+@pytest.mark.parametrize("kind", ["noise", "ties", "pan", "static"])
+def test_batched_content(orc, cairo, kind):
+    from tests import content
+
+    _run_batched(orc, cairo, 352, 288, 2, 16, 12, 6, gen=lambda w, h, t: content.make(kind, w, h, t))
+
+
 # ---------------------------------------------------------------------------
 # Whole streams through the drop-in encoder (evx1_encoder API)
 # ---------------------------------------------------------------------------
@@ -204,12 +228,13 @@ def test_encoder_stream_matches_golden(orc, cairo, cfg):
 # the GPU with row-level dependencies); every frame must still match.
 # ---------------------------------------------------------------------------
 
-def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0):
+def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None):
+    gen = gen or orc.make_frame
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
     ref = []
     for t in range(frames):
-        rgb = orc.make_frame(w, h, t)
+        rgb = gen(w, h, t)
         intra = t == 0 or (intra_every and t % intra_every == 0)
         if intra:
             e.insert_intra()
@@ -233,7 +258,7 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0):
     for t in range(frames):  # at most `stages` frames in flight (submitted, not released)
         if len(pending) == stages:
             check(*pending.pop(0))
-        pending.append((t, ctx.submit(orc.make_frame(w, h, t), t, not ref[t][0], q)))
+        pending.append((t, ctx.submit(gen(w, h, t), t, not ref[t][0], q)))
     for p in pending:
         check(*p)
     ctx.sync()
@@ -403,6 +428,10 @@ def test_decoder_intra_and_ragged(orc, cairo):
 
 def test_decoder_720p(orc, cairo):
     _decode_round_trip(orc, cairo, 1280, 720, 2, 16, 4)
+
+
+def test_decoder_4k(orc, cairo):
+    _decode_round_trip(orc, cairo, 3840, 2160, 4, 16, 3)
 
 
 def test_decoder_rejects_bad_streams(cairo):

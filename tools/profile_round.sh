@@ -1,7 +1,8 @@
 #!/bin/bash
 # Profile bench.py's hot path (run on the GPU box from the repo root):
 #   rocprofv3 --kernel-trace --stats, then FETCH_SIZE and WRITE_SIZE in their
-#   own --pmc passes (MI355X_MICROARCH.md §HBM), then tools/pmc_summary.py.
+#   own --pmc passes (MI355X_MICROARCH.md §HBM).  Only gpurun_out/ comes back
+#   from the box: run tools/pmc_summary.py here afterwards to write profiles/.
 # usage: bash tools/profile_round.sh <round> <config>
 set -e
 R=${1:-r01}; C=${2:-720p}
@@ -12,4 +13,4 @@ ARGS="--config $C --no-end-to-end --no-cpu-baseline --steps 96 --warmup 16"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_kt -o run -- python3 bench.py $ARGS > $OUT/prof_kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py $ARGS > $OUT/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1
-python3 tools/pmc_summary.py --round $R --config $C --src $OUT
+echo "profiled $R $C: now run python tools/pmc_summary.py --round $R --config $C --src gpurun_out locally"
