@@ -264,17 +264,18 @@ class Context:
 
     def read_stamps(self):
         """-> (per-MB stamps (16, hmb, wmb, 12), per-row deblock chunk stamps (16, hmb, 256),
-        engine [entry, exit], inter-task stamps (16, hmb, ng, nref, 3)) for the
-        frames of the last batch; 100 MHz ticks."""
+        engine [entry, exit], inter-task stamps (16, hmb, ng, 12): dequeue, ready,
+        done, zero-MV checked, window staged, level-2 wait start / end, level-2
+        count, step 16 done, integer steps done, sub-pel done) for the frames of the last batch; 100 MHz ticks."""
         n_mb, n_db = self.hmb * self.wmb * 12, self.hmb * 256
         fw = n_mb + n_db
-        ng, nref = (self.wmb + 3) // 4, max(self.ring - 1, 1)
-        n_it = 16 * self.hmb * ng * nref * 3
+        ng = (self.wmb + 3) // 4
+        n_it = 16 * self.hmb * ng * 12
         out = np.zeros(16 * fw + 2 + n_it, np.uint64)
         _ck(self.L.cairo_ctx_read_stamps(self.h, _ptr(out)), "read_stamps")
         fr = out[: 16 * fw].reshape(16, fw)
         return (fr[:, :n_mb].reshape(16, self.hmb, self.wmb, 12), fr[:, n_mb:].reshape(16, self.hmb, 256),
-                out[16 * fw:16 * fw + 2], out[16 * fw + 2:].reshape(16, self.hmb, ng, nref, 3))
+                out[16 * fw:16 * fw + 2], out[16 * fw + 2:].reshape(16, self.hmb, ng, 12))
 
     def set_profiling(self, enable: bool) -> None:
         _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")

@@ -132,7 +132,7 @@ PlaneSet slot_planes(int16_t* base, const cairo_ctx* c, int slot) {
 size_t stamp_words(const cairo_ctx* c) {
   // frames, engine entry/exit, then 3 stamps per inter task
   return kMaxBatch * stamp_frame_words((int)c->wmb, (int)c->hmb) + 2 +
-         (size_t)kMaxBatch * c->hmb * ((c->wmb + 3) / 4) * c->nref * 3;
+         (size_t)kMaxBatch * c->hmb * ((c->wmb + 3) / 4) * kIStamps;
 }
 
 EngineArgs engine_args(const cairo_ctx* c) {

@@ -38,6 +38,10 @@ constexpr int kStampPhases = 12;  // 10 real-time stamps + 2 shader-clock stamps
 // ...followed by kDbStamps per MB row: the deblock's publish time of each
 // column chunk; then 2 words: engine entry (min) / exit (max).
 constexpr int kDbStamps = 256;
+// ...and per (frame, row, inter group) kIStamps words: dequeue, ready, done,
+// zero-MV checked, window staged, level-2 wait start / end, level-2 count,
+// then (reference offset 1) step 16 done, integer steps done, sub-pel done.
+constexpr int kIStamps = 12;
 // Stamps of frame j of a batch start at j * stamp_frame_words; the 2 engine
 // words follow the kMaxBatch frames.
 __host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
@@ -90,7 +94,7 @@ struct FrameArgs {
   int32_t* deblocked;  // [hmb] final luma columns per MB row (monotone)
   const int32_t* prev_deblocked;  // the previous frame's, if it is in this batch (else nullptr)
   uint64_t* stamps;    // diagnostic (nullptr = off)
-  uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, 3 stamps (wait, ready, done)
+  uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, kIStamps stamps (see kernels.hip)
   const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)
 };
 

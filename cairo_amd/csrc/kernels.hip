@@ -219,6 +219,45 @@ hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Biased 16-bit storage (v ^ 0x8000): unsigned order equals signed order.
+__device__ __forceinline__ int unbias(int16_t b) { return (int)(int16_t)(b ^ (int16_t)0x8000); }
+
+// Sum / max over one 16-lane DPP row (a candidate's group); all 16 lanes get it.
+__device__ __forceinline__ int row16_sum(int v) {
+  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x122, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x121, 0xF, 0xF, false);
+  return v;
+}
+__device__ __forceinline__ int row16_max(int v) {
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x122, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x121, 0xF, 0xF, false));
+  return v;
+}
+
+// A 16-lane group evaluates one candidate: lane i owns luma row i (16 px) and
+// 4 pixels of U and V (row i>>1, columns (i&1)*4..+3).  Source pixels as
+// biased u16 pairs.
+struct SrcRow {
+  uint32_t y[8], u[2], v[2];
+};
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ int src_px(const uint32_t* p, int k) {  // unbiased pixel k
+  return unbias((int16_t)(p[k >> 1] >> (16 * (k & 1))));
+}
+
+// |src - cand| over biased pairs: SAD (v_sad_u16) and the two one-sided
+// saturated differences, whose packed maxima give the MAD.
+__device__ __forceinline__ void pk_diff(uint32_t a, uint32_t b, uint32_t& sad, u16x2& m1, u16x2& m2) {
+  sad = __builtin_amdgcn_sad_u16(a, b, sad);
+  m1 = __builtin_elementwise_max(m1, __builtin_elementwise_sub_sat(as_u16x2(a), as_u16x2(b)));
+  m2 = __builtin_elementwise_max(m2, __builtin_elementwise_sub_sat(as_u16x2(b), as_u16x2(a)));
+}
+
 // ---------------------------------------------------------------------------
 // Inter-search window in LDS, shared by the 4 waves of a workgroup that search
 // 4 horizontally adjacent macroblocks: 80 luma rows x 128 columns (origin 32 px
@@ -235,9 +274,17 @@ struct alignas(16) Window {
   int16_t v[kWinC * kWinCP];
 };
 
-// Stage the in-frame part of window rows [r0, r1) x columns [c0, c1) (luma,
-// multiples of 16; chroma the halves) with origin (ox, oy) (luma pixels,
-// multiples of 16) from plane set p.  All 256 threads participate.
+// Eight int16 as biased u16 (v ^ 0x8000: unsigned order = signed order, so
+// the candidate rows can use packed u16 SAD / saturating-difference ops).
+__device__ __forceinline__ uint4 bias4(uint4 v) {
+  v.x ^= 0x80008000u, v.y ^= 0x80008000u, v.z ^= 0x80008000u, v.w ^= 0x80008000u;
+  return v;
+}
+
+// Stage the in-frame part of window rows [r0, r1) x columns [c0, c1) (luma;
+// columns multiples of 16; chroma rows [r0/2, r1/2), columns halved) with
+// origin (ox, oy) (luma pixels, multiples of 16) from plane set p, biased.
+// All 256 threads participate.
 __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa, int ha, int ox,
                                             int oy, int r0, int r1, int c0, int c1) {
   const int nc = (c1 - c0) >> 3, nl = (r1 - r0) * nc;  // 16-B chunks per row / in all
@@ -245,10 +292,10 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
     const int r = r0 + k / nc, c = c0 + (k % nc) * 8;
     const int gy = oy + r, gx = ox + c;
     if (gy >= 0 && gy < ha && gx >= 0 && gx < wa)
-      *(int4*)&w.y[r * kWinLP + c] = *(const int4*)&p.y[(size_t)gy * wa + gx];
+      *(uint4*)&w.y[r * kWinLP + c] = bias4(*(const uint4*)&p.y[(size_t)gy * wa + gx]);
   }
   const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
-  const int ncc = nc >> 1, ncl = ((r1 - r0) >> 1) * ncc;
+  const int ncc = nc >> 1, ncl = ((r1 >> 1) - (r0 >> 1)) * ncc;  // chroma rows [r0/2, r1/2)
   for (int k = threadIdx.x; k < 2 * ncl; k += 256) {
     const int pl = k >= ncl, kk = k - pl * ncl;
     const int r = (r0 >> 1) + kk / ncc, c = (c0 >> 1) + (kk % ncc) * 8;
@@ -256,7 +303,7 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
     if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
       const int16_t* src = pick(p, 1 + pl);
       int16_t* dst = pl ? w.v : w.u;
-      *(int4*)&dst[r * kWinCP + c] = *(const int4*)&src[(size_t)gy * cw + gx];
+      *(uint4*)&dst[r * kWinCP + c] = bias4(*(const uint4*)&src[(size_t)gy * cw + gx]);
     }
   }
 }
@@ -272,12 +319,12 @@ __device__ __forceinline__ Px6 px_from_window(const Window& w, int wx, int wy) {
   const int16_t* py = &w.y[(wy + (l >> 2)) * kWinLP + wx + (l & 3) * 4];
   int cwx = wx >> 1, cwy = wy >> 1;  // caller passes window coords with the same parity as frame coords
   Px6 r;
-  r.y0 = py[0];
-  r.y1 = py[1];
-  r.y2 = py[2];
-  r.y3 = py[3];
-  r.u = w.u[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)];
-  r.v = w.v[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)];
+  r.y0 = unbias(py[0]);
+  r.y1 = unbias(py[1]);
+  r.y2 = unbias(py[2]);
+  r.y3 = unbias(py[3]);
+  r.u = unbias(w.u[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)]);
+  r.v = unbias(w.v[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)]);
   return r;
 }
 
@@ -308,6 +355,58 @@ __device__ __forceinline__ Px6 lerp6(const Px6& a, const Px6& b, int q) {
   r.u = lerp_px(a.u, b.u, q);
   r.v = lerp_px(a.v, b.v, q);
   return r;
+}
+
+// One candidate row of the inter search: a 16-lane group evaluates the
+// candidate at window position (wx, wy); lane i owns luma row i (16 px) and
+// 4 pixels of U and V (row i>>1, columns (i&1)*4..+3).  Window values and the
+// source rows are biased u16 pairs; unaligned columns are realigned with
+// v_alignbyte_b32.  Returns the candidate's SAD (luma) and MAD (luma + chroma)
+// in every lane of the group (compute_block_sad / _mad, analysis.h:42-125).
+__device__ __forceinline__ void inter_cand_row(const Window& w, int wx, int wy, int i, const SrcRow& s,
+                                               int& sad, int& mad) {
+  uint32_t sm = 0;
+  u16x2 m1 = {0, 0}, m2 = {0, 0};
+  {
+    const int sh = (wx & 1) * 2;
+    const uint32_t* row = (const uint32_t*)&w.y[(wy + i) * kWinLP] + (wx >> 1);
+    uint32_t d[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = row[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) pk_diff(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), sm, m1, m2);
+  }
+  {
+    const int cr = (wy >> 1) + (i >> 1), cc = (wx >> 1) + (i & 1) * 4, sh = (cc & 1) * 2;
+    const uint32_t* ru = (const uint32_t*)&w.u[cr * kWinCP] + (cc >> 1);
+    const uint32_t* rv = (const uint32_t*)&w.v[cr * kWinCP] + (cc >> 1);
+    const uint32_t u0 = ru[0], u1 = ru[1], u2 = ru[2], v0 = rv[0], v1 = rv[1], v2 = rv[2];
+    uint32_t dummy = 0;
+    pk_diff(s.u[0], __builtin_amdgcn_alignbyte(u1, u0, sh), dummy, m1, m2);
+    pk_diff(s.u[1], __builtin_amdgcn_alignbyte(u2, u1, sh), dummy, m1, m2);
+    pk_diff(s.v[0], __builtin_amdgcn_alignbyte(v1, v0, sh), dummy, m1, m2);
+    pk_diff(s.v[1], __builtin_amdgcn_alignbyte(v2, v1, sh), dummy, m1, m2);
+  }
+  const u16x2 m = __builtin_elementwise_max(m1, m2);
+  sad = row16_sum((int)sm);
+  mad = row16_max(max((int)m.x, (int)m.y));
+}
+
+// Biased source rows of macroblock (px, py) for lane group slot i (SrcRow layout).
+__device__ __forceinline__ SrcRow load_src_rows(const PlaneSet& in, int wa, int px, int py, int i) {
+  SrcRow s;
+  const uint4* ry = (const uint4*)(in.y + (size_t)(py + i) * wa + px);
+  const uint4 r0 = ry[0], r1 = ry[1];
+  s.y[0] = r0.x, s.y[1] = r0.y, s.y[2] = r0.z, s.y[3] = r0.w;
+  s.y[4] = r1.x, s.y[5] = r1.y, s.y[6] = r1.z, s.y[7] = r1.w;
+  const size_t co = (size_t)((py >> 1) + (i >> 1)) * (wa >> 1) + (px >> 1) + (i & 1) * 4;
+  const uint2 u2 = *(const uint2*)(in.u + co), v2 = *(const uint2*)(in.v + co);
+  s.u[0] = u2.x, s.u[1] = u2.y, s.v[0] = v2.x, s.v[1] = v2.y;
+#pragma unroll
+  for (int k = 0; k < 8; k++) s.y[k] ^= 0x80008000u;
+#pragma unroll
+  for (int k = 0; k < 2; k++) s.u[k] ^= 0x80008000u, s.v[k] ^= 0x80008000u;
+  return s;
 }
 
 // Wave-uniform SAD (luma) and MAD (luma + chroma) between src and cand
@@ -467,17 +566,21 @@ __device__ __forceinline__ BlockDesc make_desc(const Sel& s, int px, int py, int
 // `off`, one wave per macroblock, in the shared window.
 // ---------------------------------------------------------------------------
 
-// The window is staged in two levels.  Level 1, window rows [0, 64) x columns
-// [0, 112) (frame rows py-32..py+31, columns 64g-32..64g+79), covers the
-// zero-MV block, the whole first (+-16) step of every macroblock of the group
-// and any later candidate that stays there: it needs the previous frame final
-// on MB rows <= r+1 over those columns, i.e. its deblock progress of row r+2
-// (whose top edge finishes row r+1) at 64g+80.  Level 2 (the rest: the bottom
-// 16 rows and the right 16 columns) is staged only when a step could reach it,
-// after the previous frame's deblock progress of row r+3 passed 64g+96.  With
-// typical motion the search never leaves level 1, so a frame follows its
-// predecessor at MB rows r+2 / +5 macroblocks instead of r+3 / +6.
-constexpr int kLvl1Rows = 64, kLvl1Cols = 112;
+// The window is staged in three parts, each when the previous frame is final
+// over it.  The previous frame's deblock progress word of MB row k counts
+// columns whose pixel rows 16k-3 .. 16k+12 are final (rows 16k+13..15 change
+// again with row k+1's top edge, kernels.hip deblock_chunk).
+//  * Level 1, window rows [0, 77) x columns [0, 112): frame rows py-32..py+44,
+//    columns 64g-32..64g+79.  Needs progress of row r+2 at 64g+80.  It holds
+//    every candidate with a vertical offset up to +29 (the first three steps
+//    16 + 8 + 4 and more) whose columns stay inside.
+//  * Level 2c, columns [112, 128) of those rows: progress of row r+2 at
+//    64g+96 (one macroblock later), when a step of the right-hand macroblock
+//    could reach it.
+//  * Level 2r, window rows [77, 80): progress of row r+3 at 64g+96, only for a
+//    vertical offset beyond +29.
+// So a frame follows its predecessor at MB row r+2, 5-6 macroblocks ahead.
+constexpr int kLvl1Rows = 77, kLvl1Cols = 112;
 
 #ifndef CAIRO_HELPER_INTERLEAVE
 #define CAIRO_HELPER_INTERLEAVE 1
@@ -553,8 +656,8 @@ __device__ __forceinline__ int inter_need_cols(const FrameArgs& a, int g, int le
 }
 
 __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int off, InterLds& L, DbLds& D,
-                                           DbState& st, int* flag) {
-  const int wave = threadIdx.x >> 6;
+                                           DbState& st, int* flag, uint64_t* is) {
+  const int wave = uni(threadIdx.x >> 6);  // scalar: the acceptance replay runs on SGPRs
   const int x = 4 * g + wave;
   const bool valid = x < a.wmb;
   const int px = x * kMB, py = r * kMB, mb = r * a.wmb + x;
@@ -568,35 +671,45 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
   s.ssd = INT32_MAX;
   s.sp_idx = s.sp_amt = s.sp_en = 0;
   s.sad = s.mad = 0;
+  SrcRow srow;  // biased source rows of this lane's group slot (integer steps)
   if (valid) {  // zero-MV candidate straight from the planes
     src = px_from_planes(a.in, a.wa, px, py);
     sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
+    srow = load_src_rows(a.in, a.wa, px, py, threadIdx.x & 15);
   }
   const bool need = valid && s.mad >= thr;
   if ((threadIdx.x & 63) == 0) L.need[wave] = need;
   __syncthreads();
+  if (is && off == 1) is[3] = __builtin_amdgcn_s_memrealtime();
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
     const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
     load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, 0, kLvl1Cols);
     __syncthreads();
-    bool lvl2 = false;  // workgroup-uniform
+    if (is && off == 1) is[4] = __builtin_amdgcn_s_memrealtime();
+    bool lvl2c = false, lvl2r = false;  // workgroup-uniform
     // steps 16, 8, 4, 2, 1, then the sub-pel step (reach 1 around the best)
     for (int si = 0; si < 6; si++) {
       const int step = si < 5 ? kRadius >> si : 1;
-      if (!lvl2) {
+      if (!lvl2r) {
         // this wave's candidates of the step reach window rows by+step-oy+15
         // and columns bx+step-ox+15 at most
-        const bool want = need && (s.by + step - oy > kLvl1Rows - kMB || s.bx + step - ox > kLvl1Cols - kMB);
+        const int want = need ? (s.by + step - oy > kLvl1Rows - kMB) * 2 + (!lvl2c && s.bx + step - ox > kLvl1Cols - kMB)
+                              : 0;
         if ((threadIdx.x & 63) == 0) L.lvl2[si][wave] = want;
         __syncthreads();
-        if (L.lvl2[si][0] | L.lvl2[si][1] | L.lvl2[si][2] | L.lvl2[si][3]) {
-          helper_wait(a, r, min(r + 3, a.hmb - 1), inter_need_cols(a, g, 2), D, st, flag);
-          load_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
-          load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
+        const int m = L.lvl2[si][0] | L.lvl2[si][1] | L.lvl2[si][2] | L.lvl2[si][3];
+        if (m) {
+          if (is) is[5] = __builtin_amdgcn_s_memrealtime();
+          helper_wait(a, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2), D, st, flag);
+          if (m & 2) load_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
+          if (!lvl2c) load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
           __syncthreads();
-          lvl2 = true;
+          if (is) is[6] = __builtin_amdgcn_s_memrealtime(), is[7] += (m & 2) ? 0x10000 : 1;
+          lvl2c = true;
+          lvl2r = (m & 2) != 0;
         }
       }
+      if (is && off == 1 && (si == 1 || si == 5)) is[si == 1 ? 8 : 9] = __builtin_amdgcn_s_memrealtime();
       if (!need) continue;
       // The 9 (or 16) candidates of a step are independent: evaluate them all
       // first (their wave reductions overlap), then replay the sequential
@@ -604,18 +717,27 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
       // the wave-uniform results.  An out-of-frame candidate is evaluated at
       // the current best and not offered.
       if (si < 5) {
+        // Candidate c of the 3x3 in pass p (of 3) on lane group g: c = 4p + g
+        // (the last pass's groups 1..3 repeat candidate 8).  Lane c < 9 then
+        // collects candidate c (ds_bpermute from its group's first lane) and
+        // select_int replays the sequential acceptance on lanes 0..15.
         const int bx = s.bx, by = s.by;
-        int cs[9], cm[9];
+        const int lane = threadIdx.x & 63, gi = lane & 15, grp = lane >> 4;
+        int sadv = 0, madv = 0;
 #pragma unroll
-        for (int c = 0; c < 9; c++) {
+        for (int pass = 0; pass < 3; pass++) {
+          const int c = min(4 * pass + grp, 8);
           const int cx = bx + (c % 3 - 1) * step, cy = by + (c / 3 - 1) * step;
           const bool ok = in_frame(cx, cy, a.wa, a.ha);
-          sad_mad(src, px_from_window(L.win, (ok ? cx : bx) - ox, (ok ? cy : by) - oy), cs[c], cm[c]);
+          int sad, mad;
+          inter_cand_row(L.win, (ok ? cx : bx) - ox, (ok ? cy : by) - oy, gi, srow, sad, mad);
+          const int from = (16 * (lane & 3)) << 2;
+          const int vs = __builtin_amdgcn_ds_bpermute(from, sad), vm = __builtin_amdgcn_ds_bpermute(from, mad);
+          if ((gi >> 2) == pass) sadv = vs, madv = vm;
         }
-#pragma unroll
-        for (int c = 0; c < 9; c++) {
-          const int cx = bx + (c % 3 - 1) * step, cy = by + (c / 3 - 1) * step;
-          if (in_frame(cx, cy, a.wa, a.ha)) accept_int(s, cx, cy, cs[c], cm[c], px, py, thr);
+        {
+          const int cx = bx + (gi % 3 - 1) * step, cy = by + (gi / 3 - 1) * step;
+          select_int(s, gi < 9 && in_frame(cx, cy, a.wa, a.ha), cx, cy, sadv, madv, px, py, thr, lane);
         }
       } else {
         // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
@@ -642,6 +764,7 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
       }
     }
   }
+  if (is && off == 1) is[10] = __builtin_amdgcn_s_memrealtime();
   if (valid && (threadIdx.x & 63) == 0) {
     a.inter_desc[(off - 1) * mbs + mb] = make_desc(s, px, py, thr, false, off);
     a.inter_sad[(off - 1) * mbs + mb] = s.sad;
@@ -1110,7 +1233,6 @@ __device__ __forceinline__ void win_put1(RowWindow& w, int pl, int row, int col,
     if (c < kChromaTail) t[row * kCwCP + 64 + c] = b;
   }
 }
-__device__ __forceinline__ int unbias(int16_t b) { return (int)(int16_t)(b ^ (int16_t)0x8000); }
 
 // Dword k (0..191) of macroblock (mbx, mby): its address in plane set p (same
 // order as the granules, kernels.h), and its store into the window.
@@ -1126,42 +1248,6 @@ __device__ __forceinline__ void win_put_k(RowWindow& w, int oy, int mbx, int mby
     const int u = k - 128, pl = u >> 5, r = (u & 31) >> 2, d = u & 3;
     win_put2(w, 1 + pl, mby * 8 + r - (oy >> 1), mbx * 8 + 2 * d, pair);
   }
-}
-
-// Sum / max over one 16-lane DPP row (a candidate's group); all 16 lanes get it.
-__device__ __forceinline__ int row16_sum(int v) {
-  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
-  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
-  v += __builtin_amdgcn_mov_dpp(v, 0x122, 0xF, 0xF, false);
-  v += __builtin_amdgcn_mov_dpp(v, 0x121, 0xF, 0xF, false);
-  return v;
-}
-__device__ __forceinline__ int row16_max(int v) {
-  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x122, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x121, 0xF, 0xF, false));
-  return v;
-}
-
-// A 16-lane group evaluates one candidate: lane i owns luma row i (16 px) and
-// 4 pixels of U and V (row i>>1, columns (i&1)*4..+3).  Source pixels as
-// biased u16 pairs.
-struct SrcRow {
-  uint32_t y[8], u[2], v[2];
-};
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-__device__ __forceinline__ int src_px(const uint32_t* p, int k) {  // unbiased pixel k
-  return unbias((int16_t)(p[k >> 1] >> (16 * (k & 1))));
-}
-
-// |src - cand| over biased pairs: SAD (v_sad_u16) and the two one-sided
-// saturated differences, whose packed maxima give the MAD.
-__device__ __forceinline__ void pk_diff(uint32_t a, uint32_t b, uint32_t& sad, u16x2& m1, u16x2& m2) {
-  sad = __builtin_amdgcn_sad_u16(a, b, sad);
-  m1 = __builtin_elementwise_max(m1, __builtin_elementwise_sub_sat(as_u16x2(a), as_u16x2(b)));
-  m2 = __builtin_elementwise_max(m2, __builtin_elementwise_sub_sat(as_u16x2(b), as_u16x2(a)));
 }
 
 __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int cy, int i,
@@ -1658,14 +1744,14 @@ __device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds&
   DbState st{0, 0, 0, 8};
   for (int g = 0; g < a.ng; g++) {
     trace(tr, 1, g);
-    uint64_t* is = a.istamps && tid == 0 ? a.istamps + (size_t)(r * a.ng + g) * a.nref * 3 : nullptr;
-    if (is) is[0] = __builtin_amdgcn_s_memrealtime();
+    uint64_t* is = a.istamps && tid == 0 ? a.istamps + (size_t)(r * a.ng + g) * kIStamps : nullptr;
+    if (is) is[0] = __builtin_amdgcn_s_memrealtime(), is[3] = is[4] = is[5] = is[6] = is[7] = is[8] = is[9] = is[10] = 0;
     // level 1 of the group's window (inter_task); deblock meanwhile
     helper_wait(a, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
-      for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag);
+      for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is);
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1786,9 +1872,9 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.prev_deblocked = j > 0 ? e.sync + SyncLayout::deblocked(e.hmb, a.ng, j - 1) : e.prev_last_deblocked;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   {
-    const int ng = (e.wmb + 3) / 4, nref = e.ring > 1 ? e.ring - 1 : 1;
+    const int ng = (e.wmb + 3) / 4;
     a.istamps = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, e.hmb) + 2 +
-                               (size_t)j * e.hmb * ng * nref * 3
+                               (size_t)j * e.hmb * ng * kIStamps
                          : nullptr;
   }
   a.rgb = f.rgb;

@@ -75,17 +75,35 @@ print(f"  hand-off (publish -> resume) mean {lat.mean():.3f} p50 {np.median(lat)
 clk = (st[..., 11] - st[..., 10]) / np.maximum(st[..., 9] - st[..., 0], 1) * 100.0  # MHz
 print(f"  effective shader clock: mean {clk.mean():.0f} MHz")
 # inter tasks: dequeue -> ready (dependency met) -> done
-ok = ist[..., 0, 2] > 0
+ok = ist[..., 2] > 0
 if ok.any():
-    wait = (ist[..., 0, 1] - ist[..., 0, 0])[ok] / 100.0
-    run = (ist[..., 0, 2] - ist[..., 0, 1])[ok] / 100.0
+    wait = (ist[..., 1] - ist[..., 0])[ok] / 100.0
+    run = (ist[..., 2] - ist[..., 1])[ok] / 100.0
     print(f"inter tasks: {ok.sum()}  wait mean {wait.mean():.1f} us  run mean {run.mean():.1f} us p50 {np.median(run):.1f} "
           f"max {run.max():.1f}")
+    zm = (ist[..., 3] - ist[..., 1])[ok] / 100.0
+    sw = ok & (ist[..., 4] > 0)
+    l2 = ok & (ist[..., 7] > 0)
+    print(f"  ready -> zero-MV checked mean {zm.mean():.1f} us; searched groups {sw.sum()} "
+          f"({100.0 * sw.sum() / ok.sum():.0f} %): window staged after {((ist[..., 4] - ist[..., 3])[sw] / 100.0).mean():.1f} us, "
+          f"staged -> done {((ist[..., 2] - ist[..., 4])[sw] / 100.0).mean():.1f} us (p50 "
+          f"{np.median((ist[..., 2] - ist[..., 4])[sw] / 100.0):.1f})")
+    if l2.any():
+        l2r = ok & ((ist[..., 7] >> 16) > 0)
+        print(f"  level-2 groups {l2.sum()} ({100.0 * l2.sum() / ok.sum():.1f} %; rows {l2r.sum()}, columns only "
+              f"{(l2 & ~l2r).sum()}): wait+stage mean {((ist[..., 6] - ist[..., 5])[l2] / 100.0).mean():.1f} us; "
+              f"their run mean {((ist[..., 2] - ist[..., 1])[l2] / 100.0).mean():.1f} us")
+    nl2 = sw & ~l2
+    if nl2.any():
+        print(f"  level-1-only searched groups: staged -> done mean {((ist[..., 2] - ist[..., 4])[nl2] / 100.0).mean():.1f} us")
+        seg = lambda a_, b_: ((ist[..., b_] - ist[..., a_])[nl2] / 100.0).mean()  # noqa: E731
+        print(f"    staged -> step 16 done {seg(4, 8):.1f}, -> integer steps done {seg(8, 9):.1f}, -> sub-pel done "
+              f"{seg(9, 10):.1f}, -> records released {seg(10, 2):.1f} us (first reference)")
     for j in range(B):
-        okj = ist[j, ..., 0, 2] > 0
+        okj = ist[j, ..., 2] > 0
         if okj.any() and j < 4:
-            print(f"  frame {j}: inter tasks {(ist[j, ..., 0, 0][okj].min() - t0) / 100.0:8.1f} .. "
-                  f"{(ist[j, ..., 0, 2][okj].max() - t0) / 100.0:8.1f} us")
+            print(f"  frame {j}: inter tasks {(ist[j, ..., 0][okj].min() - t0) / 100.0:8.1f} .. "
+                  f"{(ist[j, ..., 2][okj].max() - t0) / 100.0:8.1f} us")
 # frame-to-frame lag of MB completion (stamp 9) at sample positions
 F = min(max(a.frame, 1), B - 1)
 if B > 2:
@@ -109,13 +127,13 @@ for j in range(min(B, 2)):
             f"k={k}: {(dbs[j, r, k] - st[j, r, k, 9]) / 100.0:.1f}" for k in ks_))
 # frame 1, row 10: per group, when its inter task became ready / was claimed / done,
 # and when the row coder reached / resumed at the group's first MB
-if B > 1 and hb > 13 and (ist[..., 0, 2] > 0).any():
+if B > 1 and hb > 13 and (ist[..., 2] > 0).any():
     r = a.row if hasattr(a, 'row') else 10
     print(f"frame {F} row {r} per group (us): ready(deblock f{F - 1} row {r + 2}) wait-start ready done | coder reach resume")
     for g in range(0, (wb + 3) // 4, 3):
         need = min(64 * g + 80, w)  # level 1 of the inter window (kernels.hip inter_need_cols)
         kk = [k for k in range(min(wb, 256)) if (16 * (k + 1) - 12 >= need or k == wb - 1)]
         ready = (dbs[F - 1, min(r + 2, hb - 1), kk[0]] - t0) / 100.0 if kk else float("nan")
-        c, rd, dn = ((ist[F, r, g, 0, k] - t0) / 100.0 for k in range(3))
+        c, rd, dn = ((ist[F, r, g, k] - t0) / 100.0 for k in range(3))
         reach, res = (st[F, r, 4 * g, 0] - t0) / 100.0, (st[F, r, 4 * g, 1] - t0) / 100.0
         print(f"  g={g:2d}: {ready:8.1f} {c:8.1f} {rd:8.1f} {dn:8.1f} | {reach:8.1f} {res:8.1f}")
