@@ -182,6 +182,13 @@ def main():
         if k is not None:
             roof["traffic"] = k
             roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+        ws = pmc.get("engine_wave_states")
+        if ws and roof["kernel"] == "engine":
+            # SQ counters of the same workload: where the engine's wave time goes
+            # (the kernel is dependency-latency-bound, not HBM-bound)
+            roof["wave_states"] = {k2: round(ws[k2], 3) for k2 in
+                                   ("waiting_frac", "issue_stalled_frac", "issuing_frac", "valu_issue_frac_of_chip")
+                                   if k2 in ws}
 
     # end-to-end: hot path + host entropy on worker threads (rank 0 reports)
     e2e = None

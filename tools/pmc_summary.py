@@ -4,6 +4,7 @@ Inputs (gpurun_out/, written by the rocprofv3 commands in DESIGN.md §Measuremen
   prof_kt/run_kernel_stats.csv          --kernel-trace --stats
   prof_fetch/run_counter_collection.csv --pmc FETCH_SIZE  (own pass)
   prof_write/run_counter_collection.csv --pmc WRITE_SIZE  (own pass)
+  prof_sq/run_counter_collection.csv    --pmc SQ_* + GRBM_GUI_ACTIVE (wave states, optional)
 
 Outputs:
   profiles/<round>_<config>_kernel_stats.csv  (copy of the stats summary)
@@ -26,15 +27,47 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"k_convert_batch": "convert", "k_engine": "engine"}
 
 
-def per_kernel(path):
+def per_kernel(path, counter=None):
     vals = {}
     for r in csv.DictReader(open(path)):
+        if counter and r.get("Counter_Name") != counter:
+            continue
         name = r["Kernel_Name"]
         for k, short in SHORT.items():
             if f"::{k}(" in name or f"::{k}<false>(" in name:
                 vals.setdefault(short, []).append(float(r["Counter_Value"]))
     # drop the first dispatch of each kernel (warm-up: intra frame, cold caches)
     return {k: v[1:] if len(v) > 1 else v for k, v in vals.items()}
+
+
+SQ = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+      "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]
+
+
+def wave_states(path):
+    """Engine wave-state breakdown from one SQ pass (MI355X_MICROARCH.md §PMC:
+    WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, quad-cycles).
+    valu_issue_frac: VALU quad-cycles x 4 over the SIMD-cycles of the dispatch
+    (GRBM_GUI_ACTIVE summed over 8 XCDs -> per-XCD cycles; 256 CUs x 4 SIMDs)."""
+    if not os.path.exists(path):
+        return None
+    med = {}
+    for c in SQ:
+        v = per_kernel(path, c).get("engine")
+        if v:
+            med[c] = statistics.median(v)
+    if "SQ_WAVE_CYCLES" not in med:
+        return None
+    wc = med["SQ_WAVE_CYCLES"]
+    out = {"median_per_dispatch": med,
+           "waiting_frac": med.get("SQ_WAIT_ANY", 0) / wc,
+           "issue_stalled_frac": med.get("SQ_WAIT_INST_ANY", 0) / wc,
+           "issuing_frac": med.get("SQ_ACTIVE_INST_ANY", 0) / wc,
+           "valu_frac_of_wave_time": med.get("SQ_ACTIVE_INST_VALU", 0) / wc}
+    if "GRBM_GUI_ACTIVE" in med:
+        cycles = med["GRBM_GUI_ACTIVE"] / 8.0
+        out["valu_issue_frac_of_chip"] = med.get("SQ_ACTIVE_INST_VALU", 0) * 4.0 / (cycles * 256 * 4)
+    return out
 
 
 def main():
@@ -66,6 +99,9 @@ def main():
         res["per_launch_hbm_bytes"][k] = int(round((2 * f + w) * 1024))
         res["per_frame_hbm_bytes"][k] = int(round((2 * f + w) * 1024 / a.batch))
         res["dispatches"][k] = min(len(fetch[k]), len(write[k]))
+    ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
+    if ws:
+        res["engine_wave_states"] = ws
     path = os.path.join(out_dir, f"pmc_{a.config}.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res["per_launch_hbm_bytes"]))

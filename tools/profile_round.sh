@@ -7,10 +7,12 @@
 set -e
 R=${1:-r01}; C=${2:-720p}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out
-rm -rf $OUT/prof_kt $OUT/prof_fetch $OUT/prof_write
+OUT=gpurun_out/prof_$C
+rm -rf $OUT && mkdir -p $OUT
 ARGS="--config $C --no-end-to-end --no-cpu-baseline --steps 96 --warmup 16"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_kt -o run -- python3 bench.py $ARGS > $OUT/prof_kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py $ARGS > $OUT/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1
-echo "profiled $R $C: now run python tools/pmc_summary.py --round $R --config $C --src gpurun_out locally"
+# wave states of the engine (8 SQ counters + GRBM_GUI_ACTIVE, one pass)
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/prof_sq -o run -- python3 bench.py $ARGS > $OUT/prof_sq.log 2>&1
+echo "profiled $R $C: now run python tools/pmc_summary.py --round $R --config $C --src gpurun_out/prof_$C locally"
