@@ -15,6 +15,20 @@
 
 namespace cairo {
 
+// The per-frame views (FrameArgs) are written by the host before a launch and
+// never during it: read them through the constant address space, so that a
+// field is fetched once (scalar loads) instead of again after every global
+// store, each refetch waiting behind the outstanding hand-off loads.
+typedef const __attribute__((address_space(4))) FrameArgs FA;
+// A plane set field of a view, as an ordinary value.
+__host__ __device__ inline PlaneSet planes(const __attribute__((address_space(4))) PlaneSet& p) {
+  PlaneSet r;
+  r.y = p.y;
+  r.u = p.u;
+  r.v = p.v;
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // Tables (generated from their definitions; checked against the oracle by the
 // parity tests).
@@ -92,7 +106,7 @@ __device__ __forceinline__ int16_t* pick(const PlaneSet& p, int pl) {
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Diagnostic timestamp (100 MHz constant clock) of phase k of macroblock mb.
-__device__ __forceinline__ void stamp(const FrameArgs& a, int mb, int k) {
+__device__ __forceinline__ void stamp(FA& a, int mb, int k) {
   if (a.stamps && threadIdx.x == 0)
     a.stamps[(size_t)mb * kStampPhases + k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -599,15 +613,15 @@ __device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
 // The row's deblock (defined below), advanced while a helper waits.
 struct DbLds;
 struct DbState;
-__device__ __forceinline__ bool deblock_chunk_ready(const FrameArgs& a, int r, const DbState& st);
-__device__ __forceinline__ void deblock_chunk(const FrameArgs& a, int r, DbLds& D, DbState& st);
-__device__ __forceinline__ bool deblock_pending(const FrameArgs& a, const DbState& st);
+__device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st);
+__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st);
+__device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st);
 
 // Helper wait (whole workgroup): until the previous frame's deblock progress
 // of MB row rr reaches need, running this row's ready deblock chunks
 // meanwhile; then acquire what the progress word released.  Bounded like
 // every wait (the error word ends it).
-__device__ __forceinline__ void helper_wait(const FrameArgs& a, int r, int rr, int need, DbLds& D,
+__device__ __forceinline__ void helper_wait(FA& a, int r, int rr, int need, DbLds& D,
                                             DbState& st, int* flag) {
   volatile int* vflag = flag;
   uint64_t t0 = 0;
@@ -651,11 +665,11 @@ struct InterLds {
 
 // Need of the group's level-1 / level-2 windows: (MB row whose deblock
 // progress counts, luma columns).
-__device__ __forceinline__ int inter_need_cols(const FrameArgs& a, int g, int level) {
+__device__ __forceinline__ int inter_need_cols(FA& a, int g, int level) {
   return min(64 * g + (level == 1 ? 80 : 96), a.wa);
 }
 
-__device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int off, InterLds& L, DbLds& D,
+__device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLds& L, DbLds& D,
                                            DbState& st, int* flag, uint64_t* is) {
   const int wave = uni(threadIdx.x >> 6);  // scalar: the acceptance replay runs on SGPRs
   const int x = 4 * g + wave;
@@ -673,9 +687,9 @@ __device__ __forceinline__ void inter_task(const FrameArgs& a, int r, int g, int
   s.sad = s.mad = 0;
   SrcRow srow;  // biased source rows of this lane's group slot (integer steps)
   if (valid) {  // zero-MV candidate straight from the planes
-    src = px_from_planes(a.in, a.wa, px, py);
+    src = px_from_planes(planes(a.in), a.wa, px, py);
     sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
-    srow = load_src_rows(a.in, a.wa, px, py, threadIdx.x & 15);
+    srow = load_src_rows(planes(a.in), a.wa, px, py, threadIdx.x & 15);
   }
   const bool need = valid && s.mad >= thr;
   if ((threadIdx.x & 63) == 0) L.need[wave] = need;
@@ -991,7 +1005,7 @@ __device__ __forceinline__ void db_line(DbLds& D, int pl, bool vert_line, int ro
     if (w[k] != v[k]) *db_px(D, pl, vert_line ? row0 + k : row0, vert_line ? col0 : col0 + k) = (int16_t)w[k];
 }
 
-__device__ __forceinline__ const uint64_t* gran_mb(const FrameArgs& a, int mbx, int mby) {
+__device__ __forceinline__ const uint64_t* gran_mb(FA& a, int mbx, int mby) {
   return a.granules + (size_t)(mby * a.wmb + mbx) * kGranuleStride;
 }
 
@@ -1003,11 +1017,11 @@ struct DbState {
 
 // Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
 // Evaluated by thread 0 only.
-__device__ __forceinline__ bool deblock_pending(const FrameArgs& a, const DbState& st) {
+__device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st) {
   return st.k < (a.wa + kDbChunk - 1) / kDbChunk;
 }
 
-__device__ __forceinline__ bool deblock_chunk_ready(const FrameArgs& a, int r, const DbState& st) {
+__device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st) {
   const int c1 = min((st.k + 1) * kDbChunk, a.wa);
   if (r > 0 && __hip_atomic_load(&a.deblocked[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1)
     return false;
@@ -1016,7 +1030,7 @@ __device__ __forceinline__ bool deblock_chunk_ready(const FrameArgs& a, int r, c
 }
 
 // Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs).
-__device__ __forceinline__ void deblock_chunk(const FrameArgs& a, int r, DbLds& D, DbState& st) {
+__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st) {
   const int tid = threadIdx.x;
   const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
   const int cw = a.wa >> 1;
@@ -1159,7 +1173,7 @@ __device__ __forceinline__ void deblock_chunk(const FrameArgs& a, int r, DbLds& 
   st.k++;
 }
 
-__device__ __forceinline__ void deblock_task(const FrameArgs& a, int r, DbLds& D) {
+__device__ __forceinline__ void deblock_task(FA& a, int r, DbLds& D) {
   DbState st{0, 0, 0, 8};
   const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
   while (st.k < nch) deblock_chunk(a, r, D, st);
@@ -1353,19 +1367,19 @@ __device__ __forceinline__ BlockDesc uni_desc(const BlockDesc& d) {
   return u;
 }
 
-__device__ __forceinline__ uint64_t* gran_at(const FrameArgs& a, int mbx, int mby, int k) {
+__device__ __forceinline__ uint64_t* gran_at(FA& a, int mbx, int mby, int k) {
   return a.granules + (size_t)(mby * a.wmb + mbx) * kGranuleStride + k;
 }
 
 // Store lane pairs (lane, lane^1) of an 8x8 block's int16 values as dwords
 // with write-through (sc1) stores: the next frame reads them back (output_cache
 // carry of copy macroblocks) on another CU.  e = element (block-major).
-__device__ __forceinline__ void coef_store_pair(const FrameArgs& a, int e, int px, int py, int value) {
+__device__ __forceinline__ void coef_store_pair(FA& a, int e, int px, int py, int value) {
   const int nb = __builtin_amdgcn_mov_dpp(value, 0xB1, 0xF, 0xF, false);  // lane ^ 1
   if (!(threadIdx.x & 1)) {
     int pl, ex, ey;
     elem_coords(e, px, py, pl, ex, ey);
-    int16_t* cp = pick(a.coef, pl);
+    int16_t* cp = pick(planes(a.coef), pl);
     __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(cp + (size_t)ey * (pl ? a.wa >> 1 : a.wa) + ex),
                        ((uint32_t)value & 0xFFFFu) | ((uint32_t)nb << 16), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1377,7 +1391,7 @@ __device__ __forceinline__ void coef_store_pair(const FrameArgs& a, int e, int p
 // kDecode: the decoder's reconstruction (decode_slice, decode.cpp:146-170) from
 // the given block table and coefficients, without the searches.
 template <bool kDecode>
-__device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, int32_t* tr) {
+__device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
@@ -1599,7 +1613,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
           const int b = wave + 4 * bi, e = b * 64 + lane;
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
-          const int sv = plane_of(a.in, pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+          const int sv = plane_of(planes(a.in), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
           cf[bi] = fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
                              has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
         }
@@ -1624,7 +1638,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
           } else {  // the decoded coefficients (the decoder's input_cache)
             int pl, ex, ey;
             elem_coords(e, px, py, pl, ex, ey);
-            qv = plane_of(a.coef, pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+            qv = plane_of(planes(a.coef), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
           }
           const int t = idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
                                   dequant_elem(e, qv, qp, intra_path));
@@ -1638,7 +1652,7 @@ __device__ __forceinline__ void code_row(const FrameArgs& a, int by, RowLds& L, 
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
           const size_t o = (size_t)ey * (pl ? cw : a.wa) + ex;
-          coef_store_pair(a, e, px, py, pick(a.coef_prev, pl)[o]);
+          coef_store_pair(a, e, px, py, pick(planes(a.coef_prev), pl)[o]);
         }
       }
       stamp(a, mb, 7);
@@ -1723,7 +1737,7 @@ struct EngineLds {
 
 // Helper decision for group g (thread 0): 1 = the inter search may run,
 // 2 = a deblock chunk is ready meanwhile, 0 = nothing yet.
-__device__ __forceinline__ int helper_decision(const FrameArgs& a, int r, int need, const DbState& st, int nch) {
+__device__ __forceinline__ int helper_decision(FA& a, int r, int need, const DbState& st, int nch) {
   const int rr = min(r + 2, a.hmb - 1);  // level 1 of the group's window (inter_task)
   if (!a.prev_deblocked ||
       __hip_atomic_load(a.prev_deblocked + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
@@ -1737,7 +1751,7 @@ __device__ __forceinline__ int helper_decision(const FrameArgs& a, int r, int ne
 // coder waits for exactly these), and the deblock of row r, chunk by chunk as
 // the coder's granules arrive (advanced whenever the inter search is waiting
 // or done).  Never blocks on its own row coder while an inter group is due.
-__device__ __forceinline__ void row_helper(const FrameArgs& a, int r, HelperLds& L, int* flag, int32_t* tr) {
+__device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag, int32_t* tr) {
   const int tid = threadIdx.x;
   const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
   volatile int* vflag = flag;
@@ -1807,7 +1821,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
       trace(e.trace, 0, 1000000 + t);
       if (t >= total) break;
       const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
-      row_helper(e.fa[j], r, L.u.helper, &L.flag, e.trace);
+      row_helper(((FA*)e.fa)[uni(j)], r, L.u.helper, &L.flag, e.trace);
       trace(e.trace, 0, 2000000 + t);
     }
   } else {
@@ -1816,7 +1830,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
       trace(e.trace, 0, 3000000 + t);
       if (t >= total) break;
       const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
-      code_row<kDecode>(e.fa[j], r, L.u.row, e.trace);
+      code_row<kDecode>(((FA*)e.fa)[uni(j)], r, L.u.row, e.trace);
       trace(e.trace, 0, 4000000 + t);
     }
   }
@@ -1825,7 +1839,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
 }
 
 __global__ __launch_bounds__(192) void k_unpack_granules(EngineArgs e, int j, PlaneSet dst) {
-  const FrameArgs& a = e.fa[j];
+  FA& a = ((FA*)e.fa)[j];
   const int mb = blockIdx.x, k = threadIdx.x;
   const int mbx = mb % a.wmb, mby = mb / a.wmb;
   const uint32_t v = (uint32_t)a.granules[(size_t)mb * kGranuleStride + k];
