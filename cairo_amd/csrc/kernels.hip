@@ -59,6 +59,25 @@ __constant__ int16_t kAlpha[32] = {0, 0, 0, 0, 0,  0,  0,  1,  1,  1,  2,  2,  3
 __constant__ int16_t kBeta[32] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 3,
                                   3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 10, 11};
 
+// LDS copies of the tables, loaded once per workgroup (load_tables): a lookup
+// with a per-lane index is then an LDS read (lgkmcnt) instead of a global load
+// whose vmcnt(0) wait would also drain the outstanding hand-off loads.
+__shared__ int16_t sLut8[64], sQmIntra[64], sQmInter[64], sAlpha[32], sBeta[32];
+
+// Whole workgroup; ends with a barrier.
+__device__ __forceinline__ void load_tables() {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    sLut8[t] = kLut8[t];
+    sQmIntra[t] = kQmIntra[t];
+    sQmInter[t] = kQmInter[t];
+  } else if (t < 96) {
+    sAlpha[t - 64] = kAlpha[t - 64];
+    sBeta[t - 64] = kBeta[t - 64];
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // Wave64 / workgroup helpers
 // ---------------------------------------------------------------------------
@@ -835,7 +854,7 @@ __device__ __forceinline__ int fdct_lane(int16_t* sa, int16_t* sb, int lane, int
     const int8v row = load_row8(&sa[r8 * 8]);
     int t = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) t += row[k] * kLut8[c8 * 8 + k];
+    for (int k = 0; k < 8; k++) t += row[k] * sLut8[c8 * 8 + k];
     t = c8 == 0 ? (t * 45) / 128 : t / 2;
     sb[c8 * 8 + r8] = (int16_t)rdiv(t, 128);  // transposed
   }
@@ -843,7 +862,7 @@ __device__ __forceinline__ int fdct_lane(int16_t* sa, int16_t* sb, int lane, int
   const int8v col = load_row8(&sb[c8 * 8]);  // column c8 of the row pass
   int t = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) t += col[k] * kLut8[r8 * 8 + k];
+  for (int k = 0; k < 8; k++) t += col[k] * sLut8[r8 * 8 + k];
   t = r8 == 0 ? (t * 45) / 128 : t / 2;
   return (int16_t)rdiv(t, 128);
 }
@@ -857,16 +876,16 @@ __device__ __forceinline__ int idct_lane(int16_t* sa, int16_t* sb, int lane, int
   __builtin_amdgcn_wave_barrier();
   {
     const int8v col = load_row8(&sa[c8 * 8]);
-    int t = ((col[0] * kLut8[r8]) * 45) / 128;
+    int t = ((col[0] * sLut8[r8]) * 45) / 128;
 #pragma unroll
-    for (int k = 1; k < 8; k++) t += (col[k] * kLut8[k * 8 + r8]) / 2;
+    for (int k = 1; k < 8; k++) t += (col[k] * sLut8[k * 8 + r8]) / 2;
     sb[r8 * 8 + c8] = (int16_t)rdiv(t, 128);
   }
   __builtin_amdgcn_wave_barrier();
   const int8v row = load_row8(&sb[r8 * 8]);
-  int t = ((row[0] * kLut8[c8]) * 45) / 128;
+  int t = ((row[0] * sLut8[c8]) * 45) / 128;
 #pragma unroll
-  for (int k = 1; k < 8; k++) t += (row[k] * kLut8[k * 8 + c8]) / 2;
+  for (int k = 1; k < 8; k++) t += (row[k] * sLut8[k * 8 + c8]) / 2;
   return rdiv(t, 128);
 }
 
@@ -894,9 +913,9 @@ __device__ __forceinline__ int16_t quant_elem(int e, int32_t c, int qp, bool int
   int b = e >> 6, k = e & 63;
   if (intra_path) {
     if (k == 0) return (int16_t)rdiv(c, b < 4 ? luma_dc_scale(qp) : chroma_dc_scale(qp));
-    return (int16_t)rdiv(rdiv(c * kQScale, kQmIntra[k]), qp << 1);
+    return (int16_t)rdiv(rdiv(c * kQScale, sQmIntra[k]), qp << 1);
   }
-  int16_t qf = (int16_t)rdiv(c * kQScale, kQmInter[k]);
+  int16_t qf = (int16_t)rdiv(c * kQScale, sQmInter[k]);
   return (int16_t)rdiv(qf - sign16(qf) * qp, qp << 1);
 }
 // inverse_quantize_macroblock (quantize.cpp:369-379): element-wise.
@@ -904,9 +923,9 @@ __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool i
   int b = e >> 6, k = e & 63;
   if (intra_path) {
     if (k == 0) return (int16_t)(v * (b < 4 ? luma_dc_scale(qp) : chroma_dc_scale(qp)));
-    return (int16_t)((2 * v * kQmIntra[k] * qp) / kQScale);
+    return (int16_t)((2 * v * sQmIntra[k] * qp) / kQScale);
   }
-  return (int16_t)(((2 * v) * kQmInter[k] * qp) / kQScale);
+  return (int16_t)(((2 * v) * sQmInter[k] * qp) / kQScale);
 }
 
 // ---------------------------------------------------------------------------
@@ -928,7 +947,7 @@ __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool i
 __device__ __forceinline__ void dfilter_reg(int* v, int qp, int strength, bool luma) {
   const int p3 = v[0], p2 = v[1], p1 = v[2], p0 = v[3], q0 = v[4], q1 = v[5], q2 = v[6], q3 = v[7];
   const int16_t dpq = (int16_t)iabs(p0 - q0), dp = (int16_t)iabs(p1 - p0), dq = (int16_t)iabs(q1 - q0);
-  if (strength == 0 || dpq >= kAlpha[qp] || dp >= kBeta[qp] || dq >= kBeta[qp]) return;
+  if (strength == 0 || dpq >= sAlpha[qp] || dp >= sBeta[qp] || dq >= sBeta[qp]) return;
   if (strength == 2) {
     v[3] = (int16_t)rdiv(p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1, 8);
     v[2] = (int16_t)rdiv(p2 + p1 + p0 + q0, 4);
@@ -1450,6 +1469,15 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
 #pragma unroll
         for (int k = 0; k < 2; k++) s.u[k] ^= 0x80008000u, s.v[k] ^= 0x80008000u;
       }
+      // this lane's source elements for the residual (used after the search)
+      int svp[2] = {0, 0};
+      if (!kDecode) {
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+          int pl, ex, ey;
+          elem_coords((wave + 4 * bi) * 64 + lane, px, py, pl, ex, ey);
+          svp[bi] = plane_of(planes(a.in), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+        }
+      }
       const bool pf3 = by >= 3 && bx + 3 < a.wmb, pf2 = by >= 2 && bx + 3 < a.wmb;
       const bool pfs = by + 1 < a.hmb && bx + 1 < a.wmb;
       uint64_t pg3 = 0, pg2 = 0;
@@ -1613,7 +1641,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
           const int b = wave + 4 * bi, e = b * 64 + lane;
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
-          const int sv = plane_of(planes(a.in), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+          const int sv = svp[bi];
           cf[bi] = fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
                              has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
         }
@@ -1810,6 +1838,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 template <bool kDecode>
 __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   __shared__ EngineLds L;
+  load_tables();
   const int b = blockIdx.x, hmb = e.hmb;
   uint64_t* ks = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, hmb) : nullptr;
   if (ks && threadIdx.x == 0)
@@ -1944,6 +1973,7 @@ __global__ __launch_bounds__(256) void k_kat_transform(const int16_t* src, const
                                                        const uint8_t* qtype, int32_t* qvar) {
   __shared__ alignas(16) int16_t sa[kMBElems], sb[kMBElems];
   __shared__ int32_t red[12];
+  load_tables();
   const int m = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t type = qtype[2 * m];
   const int quality = qtype[2 * m + 1];
