@@ -1371,6 +1371,25 @@ __device__ __forceinline__ int pred_global(const PlaneSet& p, int wa, int e, int
   return v;
 }
 
+// A block descriptor from its four words (all lanes hold the same), fields in
+// SGPRs; q_index and variance cleared as in uni_desc.  One 16-byte load per
+// descriptor instead of a load (and a wait) per field.
+__device__ __forceinline__ BlockDesc uni_desc_words(uint4 w) {
+  BlockDesc d;
+  d.block_type = (uint32_t)uni((int)w.x);
+  const uint32_t w1 = (uint32_t)uni((int)w.y), w2 = (uint32_t)uni((int)w.z), w3 = (uint32_t)uni((int)w.w);
+  d.prediction_target = (uint8_t)w1;
+  d.pad = 0;
+  d.motion_x = (int16_t)(w1 >> 16);
+  d.motion_y = (int16_t)w2;
+  d.sp_pred = (uint8_t)(w2 >> 16);
+  d.sp_amount = (uint8_t)(w2 >> 24);
+  d.sp_index = (uint8_t)w3;
+  d.q_index = 0;
+  d.variance = 0;
+  return d;
+}
+
 __device__ __forceinline__ BlockDesc uni_desc(const BlockDesc& d) {
   BlockDesc u;
   u.block_type = (uint32_t)uni((int)d.block_type);
@@ -1493,11 +1512,19 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
       int inter_sad[kMaxRing - 1];
       int ipv[kMaxRing - 1][2];
       const int nref = a.inter ? a.ring - 1 : 0;
+      uint4 idw[kMaxRing - 1];  // all records' loads issued before the first wait
+      int isw[kMaxRing - 1];
 #pragma unroll
       for (int o = 0; o < kMaxRing - 1; o++) {
         if (o >= nref) break;
-        inter_d[o] = uni_desc(a.inter_desc[o * mbs + mb]);
-        inter_sad[o] = uni(a.inter_sad[o * mbs + mb]);
+        idw[o] = *(const uint4*)&a.inter_desc[o * mbs + mb];
+        isw[o] = a.inter_sad[o * mbs + mb];
+      }
+#pragma unroll
+      for (int o = 0; o < kMaxRing - 1; o++) {
+        if (o >= nref) break;
+        inter_d[o] = uni_desc_words(idw[o]);
+        inter_sad[o] = uni(isw[o]);
         const BlockDesc& d = inter_d[o];
         const PlaneSet rp = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
                                       (a.index + a.ring - d.prediction_target) % a.ring);
@@ -1593,8 +1620,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
       } else {
         // ---- decoder (decode_slice, decode.cpp:146-170): the block desc is
         //      given; an inter type predicts from its reference slot ----
-        d = uni_desc(a.table[mb]);
-        d.q_index = (uint8_t)uni(a.table[mb].q_index);  // uni_desc leaves it to the quantizer
+        const uint4 tw = *(const uint4*)&a.table[mb];
+        d = uni_desc_words(tw);
+        d.q_index = (uint8_t)(uni((int)tw.w) >> 8);  // uni_desc leaves it to the quantizer
         if (!(d.block_type & kIntra)) {
           from_inter = true;
           const PlaneSet rp = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
