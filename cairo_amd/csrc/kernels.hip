@@ -104,7 +104,6 @@ __device__ __forceinline__ int wave_max(int v) {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // Diagnostic live trace (mapped host memory, system scope): word k of this workgroup.
-__device__ int32_t* g_trace_dummy;
 __device__ __forceinline__ void trace(int32_t* t, int k, int v) {
   if (t && threadIdx.x == 0)
     __hip_atomic_store(&t[blockIdx.x * 4 + k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -207,16 +206,6 @@ __device__ __forceinline__ int dequeue(int32_t* ticket, int* lds_slot) {
     *lds_slot = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   return *lds_slot;
-}
-
-// XCD-aware remap: the dispatcher deals workgroups round-robin over the 8
-// XCDs; give each XCD a contiguous range of tasks so neighbouring macroblocks
-// share one L2 (speed only, never correctness).
-__device__ __forceinline__ int xcd_remap(int b, int n) {
-  int per = (n + 7) >> 3;
-  int xcd = b & 7, k = b >> 3;
-  int t = xcd * per + k;
-  return t < n ? t : -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1192,12 +1181,6 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
   st.k++;
 }
 
-__device__ __forceinline__ void deblock_task(FA& a, int r, DbLds& D) {
-  DbState st{0, 0, 0, 8};
-  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
-  while (st.k < nch) deblock_chunk(a, r, D, st);
-}
-
 // ---------------------------------------------------------------------------
 // K2: the macroblock wavefront.  One workgroup owns one macroblock row at a
 // time (dequeued in order) and walks it left to right.  MB (bx, by) starts
@@ -1778,29 +1761,6 @@ struct EngineLds {
   int slot;
   int flag;  // helper decisions broadcast from thread 0 (kept out of the union)
 };
-
-// Row helper (j, r): the inter search of MB row r, group by group as the
-// previous frame becomes final over each group's search window (the row
-// coder waits for exactly these), and the deblock of row r, chunk by chunk as
-// the coder's granules arrive (advanced whenever the inter search is waiting
-// or done).  Never blocks on its own row coder while an inter group is due.
-
-// Row helper (j, r): the inter search of MB row r, group by group as the
-// previous frame becomes final over each group's search window (the row
-// coder waits for exactly these), and the deblock of row r, chunk by chunk as
-// the coder's granules arrive (advanced whenever the inter search is waiting
-// or done).  Never blocks on its own row coder while an inter group is due.
-
-// Helper decision for group g (thread 0): 1 = the inter search may run,
-// 2 = a deblock chunk is ready meanwhile, 0 = nothing yet.
-__device__ __forceinline__ int helper_decision(FA& a, int r, int need, const DbState& st, int nch) {
-  const int rr = min(r + 2, a.hmb - 1);  // level 1 of the group's window (inter_task)
-  if (!a.prev_deblocked ||
-      __hip_atomic_load(a.prev_deblocked + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
-    return 1;
-  if (kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st)) return 2;
-  return 0;
-}
 
 // Row helper (j, r): the inter search of MB row r, group by group as the
 // previous frame becomes final over each group's search window (the row
