@@ -149,7 +149,7 @@ struct EngineArgs {
 // at most on frame f-1, row r+3, so any slope > 3 keeps every wait pointing
 // to an earlier key (deadlock-free), while frames interleave in the pools
 // instead of queueing behind each other.
-constexpr int kOrderSlope = 6;
+constexpr int kOrderSlope = 5;
 
 // RGB -> YUV of every frame of the batch into its slot's source planes.
 hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);
