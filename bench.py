@@ -52,7 +52,7 @@ def parse():
                    help="entropy workers per rank (0: min(14, host CPUs / ranks - 2); the GPU box gives 16 CPUs per GPU)")
     p.add_argument("--no-end-to-end", action="store_true")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
-    p.add_argument("--batch", type=int, default=16, help="frames per engine launch (pipelined)")
+    p.add_argument("--batch", type=int, default=0, help="frames per engine launch (pipelined; 0 = library default)")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
     return p.parse_args()
 
@@ -137,7 +137,8 @@ def main():
         return base + f * stride
 
     ctx = cairo_amd.Context(w, h, ring, device=local)
-    ctx.set_batch(a.batch)
+    if a.batch:
+        ctx.set_batch(a.batch)
     if a.rows:
         ctx.set_workgroups(a.rows)
     stages = ctx.L.cairo_ctx_stages(ctx.h)
@@ -194,7 +195,8 @@ def main():
     e2e = None
     if not a.no_end_to_end:
         ctx2 = cairo_amd.Context(w, h, ring, device=local)
-        ctx2.set_batch(a.batch)
+        if a.batch:
+            ctx2.set_batch(a.batch)
         e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, barrier, dist, dev, world)
         ctx2.close()
 

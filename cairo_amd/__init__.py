@@ -36,6 +36,7 @@ BLOCK_DESC = np.dtype(
 assert BLOCK_DESC.itemsize == 16
 
 EVX_SUCCESS = 0
+MAX_BATCH = 32  # kMaxBatch (kernels.h): frames per engine launch, stamp layout
 EVX_ERROR_HARDWAREFAIL = 5
 
 
@@ -263,19 +264,19 @@ class Context:
         return y, u, v
 
     def read_stamps(self):
-        """-> (per-MB stamps (16, hmb, wmb, 12), per-row deblock chunk stamps (16, hmb, 256),
-        engine [entry, exit], inter-task stamps (16, hmb, ng, 12): dequeue, ready,
+        """-> (per-MB stamps (MAX_BATCH, hmb, wmb, 12), per-row deblock chunk stamps (MAX_BATCH, hmb, 256),
+        engine [entry, exit], inter-task stamps (MAX_BATCH, hmb, ng, 12): dequeue, ready,
         done, zero-MV checked, window staged, level-2 wait start / end, level-2
         count, step 16 done, integer steps done, sub-pel done) for the frames of the last batch; 100 MHz ticks."""
         n_mb, n_db = self.hmb * self.wmb * 12, self.hmb * 256
         fw = n_mb + n_db
         ng = (self.wmb + 3) // 4
-        n_it = 16 * self.hmb * ng * 12
-        out = np.zeros(16 * fw + 2 + n_it, np.uint64)
+        n_it = MAX_BATCH * self.hmb * ng * 12
+        out = np.zeros(MAX_BATCH * fw + 2 + n_it, np.uint64)
         _ck(self.L.cairo_ctx_read_stamps(self.h, _ptr(out)), "read_stamps")
-        fr = out[: 16 * fw].reshape(16, fw)
-        return (fr[:, :n_mb].reshape(16, self.hmb, self.wmb, 12), fr[:, n_mb:].reshape(16, self.hmb, 256),
-                out[16 * fw:16 * fw + 2], out[16 * fw + 2:].reshape(16, self.hmb, ng, 12))
+        fr = out[: MAX_BATCH * fw].reshape(MAX_BATCH, fw)
+        return (fr[:, :n_mb].reshape(MAX_BATCH, self.hmb, self.wmb, 12), fr[:, n_mb:].reshape(MAX_BATCH, self.hmb, 256),
+                out[MAX_BATCH * fw:MAX_BATCH * fw + 2], out[MAX_BATCH * fw + 2:].reshape(MAX_BATCH, self.hmb, ng, 12))
 
     def set_profiling(self, enable: bool) -> None:
         _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")

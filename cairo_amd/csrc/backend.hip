@@ -33,9 +33,13 @@ using namespace cairo;
 
 namespace {
 
-constexpr int kStages = 64;      // staging slots (frames in flight): four 16-frame batches
+constexpr int kStages = 64;      // staging slots (frames in flight): two 32-frame or four 16-frame batches
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
-constexpr int kDefaultBatch = 16;
+// Frames per launch by default: 32 for frames up to 720p (launch boundaries
+// cost a visible share there: +4 % at 720p), 16 above (4K lost 20 % at 32:
+// with frames that long, more frames per launch only spreads the workers).
+constexpr int kSmallFrameMBs = 4000;
+inline int default_batch(size_t mbs) { return mbs <= (size_t)kSmallFrameMBs ? 32 : 16; }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 constexpr int kMaxLaunchWG = 384;  // workgroups per launch: two launches fill the 768 slots (3 per CU)
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)
@@ -89,7 +93,7 @@ struct cairo_ctx {
   Stage st[kStages];
   int next_ticket = 0;
   uint32_t epoch = 0;
-  int batch_max = kDefaultBatch;
+  int batch_max = 16;
   FrameDesc pend[kMaxBatch];
   int npend = 0;
   int last_slot = -1;  // slot of the last launched frame
@@ -357,6 +361,7 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   c->ring = ring;
   c->plane_elems = (size_t)c->wa * c->ha * 3 / 2;
   c->mbs = (size_t)c->wmb * c->hmb;
+  c->batch_max = default_batch(c->mbs);
   c->nref = ring > 1 ? ring - 1 : 1;
   c->sync_words = (size_t)SyncLayout::words((int)c->hmb, (int)(c->wmb + 3) / 4);
   int r = kSuccess;

@@ -49,7 +49,7 @@ __host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
 }
 
 // Frames per engine launch.
-constexpr int kMaxBatch = 16;
+constexpr int kMaxBatch = 32;
 
 // One frame of a batch (host-filled, kernarg).
 struct FrameDesc {
