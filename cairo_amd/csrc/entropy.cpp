@@ -4,11 +4,13 @@
 // delta-DC zig-zag run-length coefficients, exp-Golomb precode, adaptive
 // binary arithmetic coder (abac.cpp).  The coder is bit-serial by
 // construction (one adaptive model per frame), so the speed comes from a
-// tight loop: table-driven exp-Golomb codes fed straight into the coder (no
-// intermediate feed buffer), a 64-bit output accumulator, and frames spread
-// over host threads by the caller.
+// short serial chain: the precode is built first as one packed feed (table-
+// driven exp-Golomb codes), then a single loop codes it with the coder state
+// in registers, no division and no data-dependent branch per symbol; frames
+// are spread over host threads by the caller (pipeline.cpp).
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "../../include/cairo_amd.h"
 #include "entropy.h"
@@ -24,6 +26,20 @@ constexpr uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25,
                                  13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43,
                                  36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45,
                                  38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Bit reversal of a byte.
+struct Rev8 {
+  uint8_t v[256];
+  constexpr Rev8() : v() {
+    for (int i = 0; i < 256; i++) {
+      int r = 0;
+      for (int b = 0; b < 8; b++) r |= ((i >> b) & 1) << (7 - b);
+      v[i] = (uint8_t)r;
+    }
+  }
+  constexpr uint8_t operator[](uint32_t i) const { return v[i]; }
+};
+constexpr Rev8 kRev8;
 
 // exp-Golomb code of v >= 1 in stream order (LSB first): (bits-1) zeros then v
 // MSB first (golomb.cpp:31-84; egtables.h holds the same codes for |v| < 256).
@@ -58,109 +74,154 @@ struct CodeTables {
 };
 const CodeTables kCodes;
 
-// LSB-first bit writer into the caller's buffer (bit_stream semantics,
-// bitstream.cpp:181-245: bits beyond write_index are left untouched).
-struct BitWriter {
-  uint8_t* data;
-  uint64_t cap_bits;
-  uint64_t pos;     // bits committed to data
-  uint64_t acc = 0; // pending bits, LSB first
-  uint32_t nacc = 0;
-  bool overflow = false;
+// Adaptive binary arithmetic coder, 16-bit precision (abac.cpp:28-348), run
+// over the whole feed of a slice in one loop with its state in registers.
+//
+// resolve_model's split floor(range * h0 / n), n = h0 + h1 (abac.cpp:78-93),
+// without a division on the serial chain: the model counts depend only on
+// the symbols, so the fixed-point ratio M = h0 * 2^47 / n (rounded up by
+// 1..3 units) is computed beside the chain, and the split is one multiply:
+// floor(range * M / 2^47).  Exact while 3 * 2^16 * n < 2^47 (n < 7e8; a slice
+// has at most 8 feed sections of 32 Mbit, n < 2^28): the overshoot
+// range * (M - h0 2^47 / n) / 2^47 stays below 1/n, the smallest nonzero
+// fractional part of range * h0 / n, and M >= h0 2^47 / n keeps exact
+// quotients.  The double estimate of h0 2^47 / n is within 2^-4 of the true
+// value, so floor(estimate) + 2 overshoots by 1..2.0625.
+//
+// resolve_encode_scaling (abac.cpp:178-224) is done in closed form, without
+// data-dependent branches (the bits are close to random, so a loop or an
+// if per output bit mispredicts about once per symbol):
+//  * shift-out: the k = clz16(low ^ high) common leading bits leave MSB first;
+//    pending underflow bits (e3, the opposite of the first one) follow the
+//    first of them;
+//  * underflow (E3): then, while low = 01.. and high = 10.., bit 14 is
+//    removed from both; that is the run of leading ones of low & ~high from
+//    bit 14, cut short where the reference's bound high <= 0xBFFD (not
+//    0xBFFF) stops it: high = 0xBFFE at the first step, or bits 13..0 of
+//    high all ones once its trailing ones reach them.
+//
+// Output bits collect MSB-first in a 64-bit accumulator; each full 32 are
+// bit-reversed into bit_stream order (LSB first, bitstream.cpp:181-245) and
+// stored to a scratch buffer with slack.  `s0` bits of the caller's first
+// byte are preloaded.  Returns the number of bits in `buf` (including the s0
+// preloaded ones; the buffer holds them rounded up to 4 bytes), or ~0 once
+// the output passes `limit`.
+inline uint32_t rev32(uint32_t x) {
+  x = __builtin_bswap32(x);
+  x = ((x & 0x0F0F0F0Fu) << 4) | ((x >> 4) & 0x0F0F0F0Fu);
+  x = ((x & 0x33333333u) << 2) | ((x >> 2) & 0x33333333u);
+  return ((x & 0x55555555u) << 1) | ((x >> 1) & 0x55555555u);
+}
 
-  inline void put(uint32_t b) {
-    acc |= (uint64_t)(b & 1u) << nacc;
-    if (++nacc == 56) flush();
-  }
-  inline void put_run(uint32_t b, uint32_t n) {
-    while (n) {
-      uint32_t k = n < 56 - nacc ? n : 56 - nacc;
-      if (b) acc |= ((k == 64 ? ~0ull : ((1ull << k) - 1)) << nacc);
-      nacc += k;
-      n -= k;
-      if (nacc == 56) flush();
-    }
-  }
-  void flush() {
-    if (!nacc) return;
-    if (pos + nacc > cap_bits) {
-      overflow = true;
-      nacc = 0;
-      acc = 0;
-      return;
-    }
-    uint32_t n = nacc;
-    uint64_t v = acc;
-    while (n) {
-      const uint32_t byte = (uint32_t)(pos >> 3), sh = (uint32_t)(pos & 7);
-      const uint32_t take = (8 - sh) < n ? (8 - sh) : n;
-      const uint32_t mask = ((1u << take) - 1u) << sh;
-      data[byte] = (uint8_t)((data[byte] & ~mask) | (((uint32_t)v << sh) & mask));
-      v >>= take;
-      n -= take;
-      pos += take;
-    }
-    acc = 0;
-    nacc = 0;
-  }
-};
-
-// Adaptive binary arithmetic coder, 16-bit precision (abac.cpp:28-348).
-struct Abac {
-  uint32_t low = 0, high = 0xFFFF, e3 = 0, h0 = 1, h1 = 1;
-  BitWriter* out;
-
-  inline void code(uint32_t bit) {
-    const uint64_t range = high - low;
-    const uint32_t mid = low + (uint32_t)((range * h0) / (h0 + h1));  // resolve_model
-    if (bit) {
-      low = mid + 1;
-      h1++;
-    } else {
-      high = mid;
-      h0++;
-    }
-    for (;;) {  // resolve_encode_scaling
-      if (((high ^ low) & 0x8000u) == 0) {
-        const uint32_t msb = high >> 15;
-        low -= msb << 15;
-        high -= msb << 15;
-        out->put(msb);
-        if (e3) {
-          out->put_run(msb ^ 1u, e3);
-          e3 = 0;
+uint64_t abac_encode(const uint64_t* feed, uint64_t nbits, uint8_t first, uint32_t s0, uint8_t* buf,
+                     const uint8_t* limit) {
+  uint32_t low = 0, high = 0xFFFF, e3 = 0, h0 = 1, n = 2;
+  uint64_t macc = 0;  // pending output, MSB first: the oldest of the mn bits is bit mn-1
+  uint32_t mn = 0;
+  uint8_t* p = buf;
+  auto spill = [&]() {  // mn >= 32
+    mn -= 32;
+    const uint32_t w = rev32((uint32_t)(macc >> mn));
+    memcpy(p, &w, 4);
+    p += 4;
+  };
+  auto put1 = [&](uint32_t bit) {
+    macc = (macc << 1) | bit;
+    if (++mn >= 32) spill();
+  };
+  for (uint32_t i = 0; i < s0; i++) put1((first >> i) & 1u);
+  for (uint64_t base = 0; base < nbits; base += 64) {
+    const uint64_t word = feed[base >> 6];
+    const uint32_t cnt = nbits - base < 64 ? (uint32_t)(nbits - base) : 64u;
+    if (p >= limit) return ~0ull;  // a word emits at most 64 * 32 bits: the slack absorbs it
+    for (uint32_t j = 0; j < cnt; j++) {
+      const uint32_t b = (uint32_t)(word >> j) & 1u;
+      const uint32_t sel = 0u - b;  // all ones for a 1 (masks, not ?: -- gcc turns those into branches)
+      const uint64_t m = (uint64_t)(int64_t)((double)(int32_t)h0 * (140737488355328.0 / (double)(int32_t)n)) + 2;  // 2^47
+      const uint32_t mid = low + (uint32_t)(((uint64_t)(high - low) * m) >> 47);  // resolve_model
+      n++;
+      h0 += b ^ 1u;
+      low = (low & ~sel) | ((mid + 1) & sel);
+      high = (high & sel) | (mid & ~sel);
+      // shift-out of the k common leading bits: b0, e3 copies of !b0, b1..b(k-1)
+      const uint32_t k = (uint32_t)__builtin_clz(((low ^ high) << 16) | 0x8000u);  // 0..16
+      if (__builtin_expect(e3 > 16, 0)) {
+        for (uint32_t i = 0; i < k; i++) {
+          const uint32_t bit = (low >> (15 - i)) & 1u;
+          put1(bit);
+          for (; i == 0 && e3; e3--) {
+            put1(bit ^ 1u);
+            if (p >= limit) return ~0ull;
+          }
         }
-      } else if (high <= 0xBFFDu && low > 0x3FFFu) {
-        high -= 0x4000u;
-        low -= 0x4000u;
-        e3++;
       } else {
-        break;
+        const uint32_t kmask = 0u - (uint32_t)(k != 0);
+        const uint32_t nrun = e3 & kmask;
+        const uint32_t top = low >> (16 - k);  // 0 for k = 0
+        const uint64_t b0 = (low >> 15) & 1u & kmask;
+        const uint64_t run = ((1ull << nrun) - 1) & (b0 - 1);
+        const uint32_t len = k + nrun;  // <= 32
+        macc = (macc << len) | (b0 << ((len - 1) & 63)) | (run << ((k - 1) & 63)) | (top & (((1u << k) - 1u) >> 1));
+        mn += len;
+        e3 -= nrun;
+        if (mn >= 32) spill();
       }
-      high = ((high << 1) & 0xFFFFu) | 1u;
-      low = (low << 1) & 0xFFFFu;
+      // underflow, from the unshifted values: the run of low = 1 / high = 0
+      // starting just below the first differing bit (bit 14 - k)
+      const uint64_t y = low & ~high;
+      const uint32_t sh = k + 49 < 63 ? k + 49 : 63;
+      uint32_t m3 = (uint32_t)__builtin_clzll(~(y << sh));
+      uint32_t t = k + (uint32_t)__builtin_ctz(~high);  // trailing ones of high after the shift-out
+      t = t < 16 ? t : 16;
+      const uint32_t lim = (14u - t) & (0u - (uint32_t)(t < 14)) & (0u - (uint32_t)((high | k) != 0xBFFEu));
+      m3 = m3 < lim ? m3 : lim;
+      e3 += m3;
+      const uint32_t s = k + m3;
+      low = (low << s) & 0x7FFFu;
+      high = 0x8000u | ((high << s) & 0x7FFFu) | ((1u << s) - 1u);
     }
   }
-  void finish() {  // flush_encoder (abac.cpp:279-310)
-    e3++;
-    const uint32_t b = low < 0x3FFFu ? 0u : 1u;
-    out->put(b);
-    out->put_run(b ^ 1u, e3);
-    e3 = 0;
+  // flush_encoder (abac.cpp:279-310)
+  e3++;
+  const uint32_t fb = low < 0x3FFFu ? 0u : 1u;
+  put1(fb);
+  for (; e3; e3--) {
+    put1(fb ^ 1u);
+    if (p >= limit) return ~0ull;
   }
-};
+  const uint64_t total = (uint64_t)(p - buf) * 8 + mn;
+  const uint32_t w = mn ? rev32((uint32_t)(macc << (32 - mn))) : 0u;
+  memcpy(p, &w, 4);
+  return total;
+}
 
-// The feed stream bounds each section to 32 Mbit of precode between empty()
-// calls (common.cpp:147); a write that would exceed it is dropped whole
-// (bitstream.cpp:206-216) and the callers ignore the error (stream.cpp:573-578).
+// The feed: the exp-Golomb precode of a slice, LSB first, all sections
+// concatenated (the coder never restarts between them).  The feed stream
+// bounds each section to 32 Mbit between empty() calls (common.cpp:147); a
+// write that would exceed it is dropped whole (bitstream.cpp:206-216) and the
+// callers ignore the error (stream.cpp:573-578).
 struct Feed {
-  Abac* coder;
+  std::vector<uint64_t>* words;
+  uint64_t cur = 0;
+  uint32_t ncur = 0;
   uint32_t used = 0;
+  uint64_t nbits = 0;
   inline void empty() { used = 0; }
-  inline void bits(uint32_t code, uint32_t len) {
+  inline void bits(uint32_t code, uint32_t len) {  // len <= 32
     if (used + len > kFeedCapacityBits) return;
     used += len;
-    for (uint32_t k = 0; k < len; k++) coder->code((code >> k) & 1u);
+    nbits += len;
+    cur |= (uint64_t)code << ncur;
+    if (ncur + len >= 64) {
+      words->push_back(cur);
+      cur = (uint64_t)code >> (64 - ncur);  // ncur > 32 here
+      ncur = ncur + len - 64;
+    } else {
+      ncur += len;
+    }
+  }
+  void close() {
+    if (ncur) words->push_back(cur);
   }
   inline void se(int16_t v) {
     const uint32_t i = (uint16_t)v;
@@ -217,10 +278,11 @@ void plane_blocks(Feed& f, const int16_t* img, uint32_t width, uint32_t height, 
 int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t ring,
                     const int16_t* cy, const int16_t* cu, const int16_t* cv, uint8_t* out,
                     uint64_t out_bits_capacity, uint64_t* bit_pos) {
-  BitWriter w{out, out_bits_capacity, *bit_pos};
-  Abac a;
-  a.out = &w;
-  Feed f{&a};
+  const uint64_t pos0 = *bit_pos;
+  if (pos0 > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
+  thread_local std::vector<uint64_t> feed_words;
+  feed_words.clear();
+  Feed f{&feed_words};
   const uint32_t count = (uint16_t)(wmb * hmb);  // uint16 block_count, serialize.cpp:321
   const uint32_t tbits = log2_u32(ring & 0xFF);  // log2((uint8)R), serialize.cpp:179
 
@@ -277,10 +339,28 @@ int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t r
   plane_blocks(f, cu, wa / 2, ha / 2, 8, table);
   plane_blocks(f, cv, wa / 2, ha / 2, 8, table);
 
-  a.finish();
-  w.flush();
-  *bit_pos = w.pos;
-  return w.overflow ? 7 /* EVX_ERROR_CAPACITY_LIMIT */ : 0;
+  f.close();
+
+  // Code the feed into scratch (bit 0 = bit 0 of the caller's byte pos0 / 8,
+  // with its bits below pos0 preloaded), then copy; bits beyond the end stay
+  // untouched.
+  const uint64_t byte0 = pos0 >> 3, cap_bytes = (out_bits_capacity + 7) / 8 - byte0;
+  constexpr uint64_t kSlack = 512;  // > the output of one 64-symbol feed word
+  thread_local std::vector<uint8_t> scratch;
+  if (scratch.size() < cap_bytes + kSlack) scratch.resize(cap_bytes + kSlack);
+  uint8_t* const buf = scratch.data();
+  const uint32_t s0 = (uint32_t)(pos0 & 7);
+  const uint64_t total = abac_encode(feed_words.data(), f.nbits, s0 ? out[byte0] : 0, s0, buf, buf + cap_bytes);
+  if (total == ~0ull || byte0 * 8 + total > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
+  const uint64_t nbits = total - s0;
+  const size_t whole = (size_t)(total >> 3);
+  memcpy(out + byte0, buf, whole);
+  if (total & 7) {
+    const uint8_t mask = (uint8_t)((1u << (total & 7)) - 1u);
+    out[byte0 + whole] = (uint8_t)((out[byte0 + whole] & ~mask) | (buf[whole] & mask));
+  }
+  *bit_pos = pos0 + nbits;
+  return 0;
 }
 
 }  // namespace cairo

@@ -118,3 +118,43 @@ def test_unserialize_round_trip(orc, cairo, ring, q, intra_every):
         for f in ("sp_amount", "sp_index"):
             np.testing.assert_array_equal(table[f][sp], et[f][sp], err_msg=f)
         np.testing.assert_array_equal(table["q_index"][~copy], et["q_index"][~copy])
+
+
+def test_serialize_at_bit_offset_and_capacity(orc, cairo):
+    """serialize_slice appends at the bit_stream's write position: any bit
+    offset gives the aligned payload shifted there, the bits before and after
+    it stay untouched (bitstream.cpp:181-245), and a capacity too small for
+    the payload is EVX_ERROR_CAPACITY_LIMIT (7)."""
+    import ctypes
+
+    w, h, ring = 176, 144, 4
+    wmb, hmb = w // 16, h // 16
+    e = orc.OracleEncoder(ring)
+    e.set_quality(16)
+    for t in range(2):
+        e.encode(orc.make_frame(w, h, t))
+    table = np.ascontiguousarray(e.block_table()).view(np.uint8)
+    y, u, v = (np.ascontiguousarray(a, dtype=np.int16) for a in e.planes(1))
+    ref, nbits = cairo.serialize_slice(e.block_table(), wmb, hmb, ring, y, u, v)
+    L = cairo.lib()
+
+    def run(buf, pos, cap):
+        p = ctypes.c_uint32(pos)
+        r = L.cairo_serialize_slice(cairo._ptr(table), wmb, hmb, ring, cairo._ptr(y), cairo._ptr(u),
+                                    cairo._ptr(v), cairo._ptr(buf), cap, ctypes.byref(p))
+        return r, p.value
+
+    rng = np.random.default_rng(3)
+    nbytes = (nbits + 7) // 8 + 16
+    for pos in (0, 1, 3, 7, 8, 13, 29):
+        buf = rng.integers(0, 256, nbytes + 8, dtype=np.uint8)
+        before = buf.copy()
+        r, end = run(buf, pos, buf.size)
+        assert r == 0 and end == pos + nbits
+        got = np.unpackbits(buf, bitorder="little")
+        want = np.unpackbits(before, bitorder="little")
+        want[pos:pos + nbits] = np.unpackbits(np.frombuffer(ref, np.uint8), bitorder="little")[:nbits]
+        np.testing.assert_array_equal(got, want, err_msg=f"pos {pos}")
+    buf = np.zeros(nbytes, np.uint8)
+    r, end = run(buf, 5, (nbits + 5) // 8 - 1)
+    assert r == 7 and end == 5
