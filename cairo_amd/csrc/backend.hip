@@ -35,11 +35,14 @@ namespace {
 
 constexpr int kStages = 64;      // staging slots (frames in flight): two 32-frame or four 16-frame batches
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
-// Frames per launch by default: 32 for frames up to 720p (launch boundaries
-// cost a visible share there: +4 % at 720p), 16 above (4K lost 20 % at 32:
-// with frames that long, more frames per launch only spreads the workers).
-constexpr int kSmallFrameMBs = 4000;
-inline int default_batch(size_t mbs) { return mbs <= (size_t)kSmallFrameMBs ? 32 : 16; }
+// Frames per launch by default, from measured sweeps (tools/batch_sweep.sh):
+// 32 for frames up to 720p (launch boundaries cost a visible share there),
+// 12 up to about 1080p (+8 % over 16: 2850 vs 2635 Mpix/s), 16 above (4K: 12
+// and 20 both lose 2-3 %, 32 loses 20 %).
+constexpr int kSmallFrameMBs = 4000, kMidFrameMBs = 16000;
+inline int default_batch(size_t mbs) {
+  return mbs <= (size_t)kSmallFrameMBs ? 32 : mbs <= (size_t)kMidFrameMBs ? 12 : 16;
+}
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 constexpr int kMaxLaunchWG = 384;  // workgroups per launch: two launches fill the 768 slots (3 per CU)
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)

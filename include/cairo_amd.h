@@ -79,7 +79,7 @@ CAIRO_API int cairo_ctx_sync(cairo_ctx *ctx);
 /* Staging slots = frames that may be in flight (submitted, not released). */
 CAIRO_API int cairo_ctx_stages(const cairo_ctx *ctx);
 /* Frames per engine launch, 1..min(32, stages/2) (default 32 for frames of up to
- * 4000 macroblocks, 16 above). */
+ * 4000 macroblocks, 12 up to 16000, 16 above). */
 CAIRO_API int cairo_ctx_set_batch(cairo_ctx *ctx, int frames);
 
 /* Introspection (synchronous; of the last submitted frame).  which: 0 input,
