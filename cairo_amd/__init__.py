@@ -79,6 +79,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
         "cairo_ctx_set_workgroups": (I, [P, I]),
         "cairo_ctx_set_batch": (I, [P, I]),
+        "cairo_default_batch": (I, [U, U]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "cairo_unserialize_slice": (I, [P, ctypes.POINTER(U), U, U, U, U, P, P, P, P]),
@@ -292,6 +293,11 @@ class Context:
 
     def set_workgroups(self, rows: int = 0) -> None:
         _ck(self.L.cairo_ctx_set_workgroups(self.h, rows), "set_workgroups")
+
+
+def default_batch(width: int, height: int) -> int:
+    """Frames per engine launch the library uses by default for this frame size."""
+    return int(lib().cairo_default_batch(width, height))
 
 
 def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):

@@ -447,6 +447,11 @@ int cairo_ctx_reset(cairo_ctx* c) {
 
 int cairo_ctx_stages(const cairo_ctx*) { return kStages; }
 
+int cairo_default_batch(uint32_t width, uint32_t height) {
+  if (!width || !height) return 0;
+  return default_batch((size_t)((width + 15) / 16) * ((height + 15) / 16));
+}
+
 int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
   if (!c || frames < 1 || frames > kMaxBatch || frames > kStages / 2) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);

@@ -81,6 +81,9 @@ CAIRO_API int cairo_ctx_stages(const cairo_ctx *ctx);
 /* Frames per engine launch, 1..min(32, stages/2) (default 32 for frames of up to
  * 4000 macroblocks, 12 up to 16000, 16 above). */
 CAIRO_API int cairo_ctx_set_batch(cairo_ctx *ctx, int frames);
+/* The default frames per launch for a frame size (no device needed; 0 for an
+ * empty size). */
+CAIRO_API int cairo_default_batch(uint32_t width, uint32_t height);
 
 /* Introspection (synchronous; of the last submitted frame).  which: 0 input,
  * 1 output_cache, 2+k ring slot k. */

@@ -21,6 +21,7 @@ import csv
 import json
 import os
 import shutil
+import sys
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -75,8 +76,16 @@ def main():
     ap.add_argument("--round", default="r01")
     ap.add_argument("--config", default="720p")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
-    ap.add_argument("--batch", type=int, default=16, help="frames per engine launch in the profiled run")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per engine launch in the profiled run (0: the library default for --config)")
     a = ap.parse_args()
+    if a.batch <= 0:
+        sys.path.insert(0, ROOT)
+        import cairo_amd
+        from bench import CONFIGS
+
+        w, h = CONFIGS[a.config][:2]
+        a.batch = cairo_amd.default_batch(w, h)
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     stats = os.path.join(a.src, "prof_kt", "run_kernel_stats.csv")
@@ -99,6 +108,13 @@ def main():
         res["per_launch_hbm_bytes"][k] = int(round((2 * f + w) * 1024))
         res["per_frame_hbm_bytes"][k] = int(round((2 * f + w) * 1024 / a.batch))
         res["dispatches"][k] = min(len(fetch[k]), len(write[k]))
+    trace = os.path.join(a.src, "prof_kt", "run_kernel_trace.csv")
+    if os.path.exists(trace):  # engine time per frame, to set beside bench.py's roofline.avg_ms
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
+                if "::k_engine<false>(" in r["Kernel_Name"]]
+        if len(durs) > 2:
+            full = durs[1:-1]  # without the first (intra frame) and the last (partial) launch
+            res["engine_ms_per_frame_rocprof"] = round(statistics.median(full) / 1e6 / a.batch, 4)
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws
