@@ -50,3 +50,12 @@ def test_bitstream_semantics(cairo):
 def test_band4_product_generator_matches_oracle(orc, cairo):
     for t in (0, 3):
         assert np.array_equal(cairo.make_band4(96, 64, t), orc.make_frame(96, 64, t))
+
+
+def test_default_batch(cairo):
+    """Frames per launch by frame size (backend.hip default_batch; DESIGN.md §4.2 sweeps)."""
+    assert cairo.default_batch(352, 288) == 32
+    assert cairo.default_batch(1280, 720) == 32
+    assert cairo.default_batch(1920, 1080) == 12
+    assert cairo.default_batch(3840, 2160) == 16
+    assert cairo.default_batch(0, 720) == 0
