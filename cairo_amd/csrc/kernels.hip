@@ -119,6 +119,15 @@ __device__ __forceinline__ int16_t* pick(const PlaneSet& p, int pl) {
   return pl == 0 ? y : (pl == 1 ? u : v);
 }
 
+// v, opaque to the optimiser: per-lane address math derived from it is
+// recomputed where it is used instead of being hoisted out of the macroblock
+// loop and kept live across the searches (where it was spilled to scratch,
+// and each reload's vmcnt wait also waited for the outstanding hand-off loads).
+__device__ __forceinline__ int fresh(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // A value every lane holds identically, moved to an SGPR so that the code
 // consuming it is scalar (no exec-mask divergence).
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -766,22 +775,22 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
         const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
         s.sp_idx = s.sp_amt = s.sp_en = 0;
         const int bx = s.bx, by = s.by;
-        int cs[16], cm[16];
+        // accepted in the order they are evaluated (neighbour-major, half
+        // then quarter), each as soon as its sums exist: no array of 16
+        // results stays live (it pushed the engine into scratch spills)
 #pragma unroll
         for (int n = 0; n < 8; n++) {
-          const int k9 = n < 4 ? n : n + 1, tx = bx + k9 % 3 - 1, ty = by + k9 / 3 - 1;
+          const int k9 = n < 4 ? n : n + 1, i = k9 % 3 - 1, j = k9 / 3 - 1, tx = bx + i, ty = by + j;
           const bool ok = in_frame(tx, ty, a.wa, a.ha);
           const Px6 nb = px_from_window(L.win, (ok ? tx : bx) - ox, (ok ? ty : by) - oy);
+          int cs[2], cm[2];
 #pragma unroll
-          for (int q = 0; q < 2; q++) sad_mad(src, lerp6(best, nb, q), cs[2 * n + q], cm[2 * n + q]);
-        }
+          for (int q = 0; q < 2; q++) sad_mad(src, lerp6(best, nb, q), cs[q], cm[q]);
+          if (ok) {
+            const int idx = frac_index(i, j);
 #pragma unroll
-        for (int n = 0; n < 8; n++) {
-          const int k9 = n < 4 ? n : n + 1, i = k9 % 3 - 1, j = k9 / 3 - 1;
-          if (!in_frame(bx + i, by + j, a.wa, a.ha)) continue;
-          const int idx = frac_index(i, j);
-#pragma unroll
-          for (int q = 0; q < 2; q++) accept_sub(s, idx, q, cs[2 * n + q], cm[2 * n + q], thr);
+            for (int q = 0; q < 2; q++) accept_sub(s, idx, q, cs[q], cm[q], thr);
+          }
         }
       }
     }
@@ -1258,6 +1267,7 @@ __device__ __forceinline__ const int16_t* win_src(const PlaneSet& p, int wa, int
   return pick(p, 1 + pl) + (size_t)(mby * 8 + r) * (wa >> 1) + mbx * 8 + 2 * d;
 }
 __device__ __forceinline__ void win_put_k(RowWindow& w, int oy, int mbx, int mby, int k, uint32_t pair) {
+  k = fresh(k);
   if (k < 128) {
     win_put2(w, 0, mby * 16 + (k >> 3) - oy, mbx * 16 + 2 * (k & 7), pair);
   } else {
@@ -1399,7 +1409,7 @@ __device__ __forceinline__ void coef_store_pair(FA& a, int e, int px, int py, in
   const int nb = __builtin_amdgcn_mov_dpp(value, 0xB1, 0xF, 0xF, false);  // lane ^ 1
   if (!(threadIdx.x & 1)) {
     int pl, ex, ey;
-    elem_coords(e, px, py, pl, ex, ey);
+    elem_coords(fresh(e), px, py, pl, ex, ey);
     int16_t* cp = pick(planes(a.coef), pl);
     __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(cp + (size_t)ey * (pl ? a.wa >> 1 : a.wa) + ex),
                        ((uint32_t)value & 0xFFFFu) | ((uint32_t)nb << 16), __ATOMIC_RELAXED,
@@ -1470,15 +1480,6 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
         for (int k = 0; k < 8; k++) s.y[k] ^= 0x80008000u;
 #pragma unroll
         for (int k = 0; k < 2; k++) s.u[k] ^= 0x80008000u, s.v[k] ^= 0x80008000u;
-      }
-      // this lane's source elements for the residual (used after the search)
-      int svp[2] = {0, 0};
-      if (!kDecode) {
-        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
-          int pl, ex, ey;
-          elem_coords((wave + 4 * bi) * 64 + lane, px, py, pl, ex, ey);
-          svp[bi] = plane_of(planes(a.in), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
-        }
       }
       const bool pf3 = by >= 3 && bx + 3 < a.wmb, pf2 = by >= 2 && bx + 3 < a.wmb;
       const bool pfs = by + 1 < a.hmb && bx + 1 < a.wmb;
@@ -1619,6 +1620,17 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
         }
       }
       stamp(a, mb, 5);
+      // this lane's source elements for the residual, loaded after the
+      // searches: live across them, they pushed the engine into scratch
+      // spills
+      int svp[2] = {0, 0};
+      if (!kDecode) {
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+          int pl, ex, ey;
+          elem_coords((wave + 4 * bi) * 64 + lane, px, py, pl, ex, ey);
+          svp[bi] = plane_of(planes(a.in), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+        }
+      }
 
       // ---- per-wave 8x8 blocks (encode_block encode.cpp:69-163,
       //      decode_block decode.cpp:15-144) ----
