@@ -1305,30 +1305,58 @@ __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int
   mad = row16_max(max((int)m.x, (int)m.y));
 }
 
-// Sub-pel candidate: lerp of the best block (bx, by) toward neighbour (tx, ty).
+// lerp_px on both halves of two biased u16 pairs; the result as a biased pair.
+__device__ __forceinline__ uint32_t lerp_pair(uint32_t pa, uint32_t pb, int q) {
+  const uint32_t ua = pa ^ 0x80008000u, ub = pb ^ 0x80008000u;
+  const int l0 = lerp_px((int16_t)ua, (int16_t)ub, q);
+  const int l1 = lerp_px((int16_t)(ua >> 16), (int16_t)(ub >> 16), q);
+  return (((uint32_t)l0 & 0xFFFFu) | ((uint32_t)l1 << 16)) ^ 0x80008000u;
+}
+
+// Sub-pel candidate: lerp of the best block (bx, by) toward neighbour (tx, ty),
+// read like cand_row (aligned dwords of the circular window and its
+// duplicated tail, realigned by v_alignbyte_b32); the lerped pairs are
+// re-biased so that SAD and MAD use the same packed u16 ops.
 __device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, int by, int tx,
                                            int ty, int q, int i, const SrcRow& s, int& sad,
                                            int& mad) {
-  const int16_t* ra = &w.y[(by + i - oy) * kCwLP];
-  const int16_t* rb = &w.y[(ty + i - oy) * kCwLP];
-  int sm = 0, mx = 0;
+  uint32_t sm = 0;
+  u16x2 m1 = {0, 0}, m2 = {0, 0};
+  {
+    const int ca = bx & 127, cb = tx & 127, sha = (ca & 1) * 2, shb = (cb & 1) * 2;
+    const uint32_t* ra = (const uint32_t*)&w.y[(by + i - oy) * kCwLP] + (ca >> 1);
+    const uint32_t* rb = (const uint32_t*)&w.y[(ty + i - oy) * kCwLP] + (cb >> 1);
+    uint32_t da[9], db[9];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int d = abs(src_px(s.y, k) - lerp_px(unbias(ra[(bx + k) & 127]), unbias(rb[(tx + k) & 127]), q));
-    sm += d;
-    mx = max(mx, d);
-  }
-  const int ca = (by >> 1) + (i >> 1) - (oy >> 1), cb = (ty >> 1) + (i >> 1) - (oy >> 1);
-  const int xa = (bx >> 1) + (i & 1) * 4, xb = (tx >> 1) + (i & 1) * 4;
+    for (int k = 0; k < 9; k++) da[k] = ra[k], db[k] = rb[k];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    mx = max(mx, abs(src_px(s.u, k) - lerp_px(unbias(w.u[ca * kCwCP + ((xa + k) & 63)]),
-                                              unbias(w.u[cb * kCwCP + ((xb + k) & 63)]), q)));
-    mx = max(mx, abs(src_px(s.v, k) - lerp_px(unbias(w.v[ca * kCwCP + ((xa + k) & 63)]),
-                                              unbias(w.v[cb * kCwCP + ((xb + k) & 63)]), q)));
+    for (int k = 0; k < 8; k++)
+      pk_diff(s.y[k],
+              lerp_pair(__builtin_amdgcn_alignbyte(da[k + 1], da[k], sha),
+                        __builtin_amdgcn_alignbyte(db[k + 1], db[k], shb), q),
+              sm, m1, m2);
   }
-  sad = row16_sum(sm);
-  mad = row16_max(mx);
+  {
+    const int ra = (by >> 1) + (i >> 1) - (oy >> 1), rb = (ty >> 1) + (i >> 1) - (oy >> 1);
+    const int xa = ((bx >> 1) + (i & 1) * 4) & 63, xb = ((tx >> 1) + (i & 1) * 4) & 63;
+    const int sha = (xa & 1) * 2, shb = (xb & 1) * 2;
+    uint32_t dummy = 0;
+#pragma unroll
+    for (int pl = 0; pl < 2; pl++) {
+      const int16_t* t = pl ? w.v : w.u;
+      const uint32_t* pa = (const uint32_t*)&t[ra * kCwCP] + (xa >> 1);
+      const uint32_t* pb = (const uint32_t*)&t[rb * kCwCP] + (xb >> 1);
+      const uint32_t a0 = pa[0], a1 = pa[1], a2 = pa[2], b0 = pb[0], b1 = pb[1], b2 = pb[2];
+      const uint32_t* sp = pl ? s.v : s.u;
+      pk_diff(sp[0], lerp_pair(__builtin_amdgcn_alignbyte(a1, a0, sha), __builtin_amdgcn_alignbyte(b1, b0, shb), q),
+              dummy, m1, m2);
+      pk_diff(sp[1], lerp_pair(__builtin_amdgcn_alignbyte(a2, a1, sha), __builtin_amdgcn_alignbyte(b2, b1, shb), q),
+              dummy, m1, m2);
+    }
+  }
+  const u16x2 m = __builtin_elementwise_max(m1, m2);
+  sad = row16_sum((int)sm);
+  mad = row16_max(max((int)m.x, (int)m.y));
 }
 
 __device__ __forceinline__ bool intra_valid(int cx, int cy, int px, int py, int wa, int ha) {
