@@ -9,13 +9,14 @@ SRC      = cairo_amd/csrc
 OBJ      = build/obj
 LIB      = cairo_amd/_lib/libcairo_amd.so
 ORACLE   = oracle/liboracle.so
+API_BIN  = cairo_amd/_lib/evx1_api_caller
 
 HIP_SRCS = $(SRC)/kernels.hip $(SRC)/backend.hip
 CPP_SRCS = $(SRC)/entropy.cpp $(SRC)/bitstream.cpp $(SRC)/encoder.cpp $(SRC)/decoder.cpp $(SRC)/pipeline.cpp $(SRC)/unserialize.cpp
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
 HDRS     = $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(ORACLE) $(API_BIN)
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -35,11 +36,15 @@ $(LIB): $(OBJS)
 	@mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
 
+# A C++ caller of the drop-in evx1_encoder API (tests and bench.py's api_encode leg).
+$(API_BIN): tests/api/evx1_api_caller.cpp include/evx1.h include/bitstream.h include/cairo_amd.h $(LIB)
+	$(CXX) -O2 -std=c++17 -Wall -o $@ $< -L$(dir $(LIB)) -lcairo_amd -Wl,-rpath,'$$ORIGIN'
+
 # Test infrastructure only (tests/, smoke(), bench.py cpu_baseline).
 $(ORACLE): oracle/evx_oracle.c oracle/evx_oracle.h
 	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ oracle/evx_oracle.c -lm
 
 clean:
-	rm -rf build $(LIB) $(ORACLE)
+	rm -rf build $(LIB) $(ORACLE) $(API_BIN)
 
 .PHONY: all clean

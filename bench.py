@@ -1,28 +1,41 @@
 """bench.py -- encoded Mpixels/s of the EVX-1 encode hot path on MI355X.
 
-Metric (BASELINE.json): encoded Mpixels/s (p-frame, q=16), bit-exact vs ref.
-Workload (BASELINE.json configs[1]): 1280x720, p-frame with 1 reference
-(ring R = 2), quality 16, band4 synthetic content (seed 1234).
+Metric (BASELINE.json): encoded Mpixels/s (p-frame, q=16), bit-exact.
+Workload (default, BASELINE.json configs[3] on one GPU): 3840x2160 P-frames,
+ring R = 4 (3 inter references), quality 16, band4 synthetic content
+(seed 1234).  --config 720p / 1080p run configs[1] / configs[2].
 
-A step = one P-frame through the hot path: RGB->YUV, inter search, the
-macroblock wavefront (intra search, classify, transform, VAQ, quantize,
-reconstruct, in-loop deblock), and the block table + coefficients handed to host
-memory for the entropy stage.  All input frames are resident in HBM before the
-timed region.  The host entropy stage (outside the hot path by design) is
-measured separately (end_to_end) and the output is checked bit-exact against
-the oracle on the cpu_baseline sample.
+A step = one engine launch's batch of P-frames (the library's default frames
+per launch for the frame size: 16 at 4K, 12 at 1080p, 32 at 720p) through the
+hot path: RGB->YUV, inter search, the macroblock wavefront (intra search,
+classify, transform, VAQ, quantize, reconstruct, in-loop deblock), and each
+frame's block table + coefficients handed to host memory for the entropy
+stage.  --steps 20 therefore times 320 4K frames.  All input frames are
+resident in HBM before the timed region.
+
+Other legs (rank 0, N = 1), outside the timed region:
+  bit_exact   the first frames of the timed context itself (same launches,
+              same batch) and of the end-to-end pipeline, serialized and
+              compared frame by frame with the oracle (test infrastructure)
+  end_to_end  hot path + host entropy on native worker threads (cairo_stream)
+  api_encode  evx1_encoder::encode() through the drop-in C++ API, called by a
+              C++ program built against include/evx1.h (one frame per call,
+              host RGB in, bitstream out: the reference's own interface)
+  cpu_baseline  the oracle (C restatement) on one host core, bounded sample
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank encodes its
-own stream (the path has no cross-stream exchange), value = aggregate.
+own stream (replicas, weak scaling: DESIGN.md §6), value = aggregate.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from collections import deque
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -31,34 +44,42 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # name: (width, height, ring, quality, BASELINE.json configs index)
-    "720p": (1280, 720, 2, 16, 1),
-    "1080p": (1920, 1080, 4, 8, 2),
     "4k": (3840, 2160, 4, 16, 3),
+    "1080p": (1920, 1080, 4, 8, 2),
+    "720p": (1280, 720, 2, 16, 1),
     "cif": (352, 288, 4, 16, 0),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# VALU: 256 CUs x 4 SIMDs x 32 lanes/clock x 2.4 GHz = 78.6 T lane-ops/s
+# (MI355X_MICROARCH.md: wave64 issues over 2 clocks); packed 16-bit ops
+# (v_sad_u16, v_pk_sub_u16, v_pk_max_u16) do 2 pixel-ops per lane.
+VALU_PEAK_PIXEL_OPS = 256 * 4 * 32 * 2.4e9 * 2
+# the reference on one Xeon core (P-frame steady state), Mpix/s
+REF_CPU_MPIX = {"4k": 1.82, "1080p": 1.61, "720p": 3.56}
+API_BIN = os.path.join(ROOT, "cairo_amd", "_lib", "evx1_api_caller")
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=300, help="timed P-frames (BASELINE configs: 300-frame IPPP streams)")
-    p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--config", default="720p", choices=sorted(CONFIGS))
+    p.add_argument("--steps", type=int, default=20, help="timed steps (engine launches of the default batch)")
+    p.add_argument("--warmup", type=int, default=3, help="untimed steps before (frame 0 is the I-frame)")
+    p.add_argument("--config", default="4k", choices=sorted(CONFIGS))
     p.add_argument("--cpu-frames", type=int, default=0,
-                   help="P-frames in the bounded CPU baseline sample (0 = about 60 Mpixels: 10-20 s of one core)")
+                   help="P-frames in the bounded CPU baseline sample (0 = about 60 Mpixels: 10-30 s of one core)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--entropy-threads", type=int, default=0,
                    help="entropy workers per rank (0: min(14, host CPUs / ranks - 2); the GPU box gives 16 CPUs per GPU)")
     p.add_argument("--no-end-to-end", action="store_true")
+    p.add_argument("--no-api", action="store_true")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
-    p.add_argument("--batch", type=int, default=0, help="frames per engine launch (pipelined; 0 = library default)")
+    p.add_argument("--batch", type=int, default=0, help="frames per engine launch (0 = library default)")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
     return p.parse_args()
 
 
 def algorithmic_bytes(w, h, ring):
-    """bytes per frame, P = one int16 YUV420 plane set."""
+    """HBM bytes per frame, P = one int16 YUV420 plane set."""
     wa, ha = (w + 15) & ~15, (h + 15) & ~15
     P = 3 * wa * ha
     return {
@@ -81,30 +102,71 @@ def max_over_ranks(x: float, dist, device) -> float:
     return float(t.item())
 
 
-def aggregate_mpix(w: int, h: int, steps: int, world: int, elapsed_max: float) -> float:
-    """Whole-job throughput: every rank encodes `steps` frames of w x h (weak scaling)."""
-    return w * h * steps * world / elapsed_max / 1e6
+def aggregate_mpix(w: int, h: int, frames: int, world: int, elapsed_max: float) -> float:
+    """Whole-job throughput: every rank encodes `frames` frames of w x h (weak scaling)."""
+    return w * h * frames * world / elapsed_max / 1e6
 
 
-def run_hot_path(ctx, dev_frames, frame_ptr, first, count, quality, stages, entropy=None):
-    """Submit frames [first, first+count) with up to `stages` in flight."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def host_cpus() -> int:
+    """CPUs this process may use (the GPU box's container quota, not the host's count)."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            return max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0))
+
+
+def frame_header(w, h, ring, q, t, intra):
+    """The stream bytes encode() writes before frame t's payload: the 14-byte
+    header on the first frame (byte 7 = 0), then the 10-byte frame descriptor
+    (evx1enc.cpp:104-131, common.h:50-76)."""
+    import struct
+
+    hdr = struct.pack("<4sHBxHHH", b"EVX1", 14, ring, (2 << 8) | 47, w, h) if t == 0 else b""
+    return hdr + struct.pack("<IIH", 0 if intra else 1, t, q)
+
+
+def record(cairo_amd, w, h, ring, q, t, payload, nbits):
+    """Frame t's stream record (header/descriptor + payload) -> (bytes, bits)."""
+    head = frame_header(w, h, ring, q, t, t == 0)
+    buf = np.zeros(len(head) + len(payload) + 16, np.uint8)
+    pos = cairo_amd.bits_append(buf, 0, head, len(head) * 8)
+    pos = cairo_amd.bits_append(buf, pos, payload, nbits)
+    return buf[: (pos + 7) // 8].tobytes(), pos
+
+
+def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None):
+    """Submit frames [first, first+count) with up to `stages` in flight;
+    on_frame(index, outputs) sees a frame's outputs before its release."""
     inflight = deque()
+
+    def retire():
+        f, t = inflight.popleft()
+        out = ctx.wait(t, copy=False)
+        if on_frame is not None:
+            on_frame(f, out)
+        ctx.release(t)
+
     for f in range(first, first + count):
         if len(inflight) == stages:
-            t = inflight.popleft()
-            out = ctx.wait(t, copy=False)
-            if entropy is not None:
-                entropy(t, out)
-            else:
-                ctx.release(t)
-        inflight.append(ctx.submit(frame_ptr(f), f, f > 0, quality, on_device=True))
+            retire()
+        inflight.append((f, ctx.submit(frame_ptr(f), f, f > 0, quality, on_device=True)))
     while inflight:
-        t = inflight.popleft()
-        out = ctx.wait(t, copy=False)
-        if entropy is not None:
-            entropy(t, out)
-        else:
-            ctx.release(t)
+        retire()
 
 
 def main():
@@ -125,80 +187,120 @@ def main():
     import cairo_amd
 
     w, h, ring, q, cfg_idx = CONFIGS[a.config]
-    nframes = a.warmup + a.steps
-    # synthetic input, uploaded to HBM before timing
-    host = np.empty((nframes, h, w, 3), np.uint8)
-    for f in range(nframes):
-        host[f] = cairo_amd.make_band4(w, h, f)
-    frames = torch.from_numpy(host).to(dev)
+    batch = a.batch or cairo_amd.default_batch(w, h)
+    warm_frames, timed_frames = a.warmup * batch, a.steps * batch
+    nframes = warm_frames + timed_frames
+    # synthetic input, generated on host threads and uploaded to HBM before timing
+    frames = torch.empty((nframes, h, w, 3), dtype=torch.uint8, device=dev)
+    chunk = 16
+    with ThreadPoolExecutor(max(1, min(8, host_cpus()))) as pool:
+        for c0 in range(0, nframes, chunk):
+            n = min(chunk, nframes - c0)
+            host = np.stack(list(pool.map(lambda f: cairo_amd.make_band4(w, h, f), range(c0, c0 + n))))
+            frames[c0:c0 + n].copy_(torch.from_numpy(host))
+    torch.cuda.synchronize()
     base, stride = frames.data_ptr(), w * h * 3
 
     def frame_ptr(f):
         return base + f * stride
 
     ctx = cairo_amd.Context(w, h, ring, device=local)
-    if a.batch:
-        ctx.set_batch(a.batch)
+    ctx.set_batch(batch)
     if a.rows:
         ctx.set_workgroups(a.rows)
-    stages = ctx.L.cairo_ctx_stages(ctx.h)
+    stages = ctx.stages
 
     def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
 
-    # warmup: frame 0 (I) + P-frames 1..W-1
-    run_hot_path(ctx, frames, frame_ptr, 0, a.warmup, q, stages)
+    # the frames the bit-exact check compares (rank 0, N = 1: the oracle's sample)
+    check = rank == 0 and world == 1 and not a.no_cpu_baseline
+    n_check = (a.cpu_frames or max(2, min(48, int(60e6 / (w * h))))) + 1 if check else 0
+    n_check = min(n_check, warm_frames)
+    hot_records = {}
+
+    def keep_record(f, out):
+        if f < n_check:
+            data, nbits = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, out.coef_y, out.coef_u,
+                                                    out.coef_v)
+            hot_records[f] = record(cairo_amd, w, h, ring, q, f, data, nbits)
+
+    # warmup: frame 0 (I) + P-frames, in the same context and launches as the timed region
+    run_hot_path(ctx, frame_ptr, 0, warm_frames, q, stages, keep_record)
     ctx.sync()
     ctx.set_profiling(True)
     ctx.take_timings()
     barrier()
     t0 = time.perf_counter()
-    run_hot_path(ctx, frames, frame_ptr, a.warmup, a.steps, q, stages)
+    run_hot_path(ctx, frame_ptr, warm_frames, timed_frames, q, stages)
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms, kframes = ctx.take_timings()
+    launches = max(1, a.steps)
     ctx.set_profiling(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
-    value = aggregate_mpix(w, h, a.steps, world, elapsed)
-    # per-frame kernel time: the engine encodes a batch of frames per launch
-    per_kernel = {"convert": kernel_ms[0] / max(kframes, 1), "engine": kernel_ms[2] / max(kframes, 1)}
+    value = aggregate_mpix(w, h, timed_frames, world, elapsed)
+    kf = max(kframes, 1)
     abytes = algorithmic_bytes(w, h, ring)
-    dominant = max(per_kernel, key=per_kernel.get)
-
-    def roofline(kernel):
-        ms = per_kernel[kernel]
-        ach = abytes[kernel] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "algorithmic_bytes": abytes[kernel],
-                "avg_ms": round(ms, 4), "per": "frame (engine launches cover a batch of frames)"}
-
-    roof = roofline(dominant)
+    engine_busy_ms = kernel_ms[3] / kf  # union of the launch intervals / frames
+    roof = {
+        "kernel": "k_engine", "bound": "hbm",
+        "achieved": round(abytes["engine"] / (engine_busy_ms * 1e-3) / 1e9, 2),
+        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": None, "traffic": None,
+        "algorithmic_bytes": abytes["engine"], "per": "frame",
+        "engine_busy_ms_per_frame": round(engine_busy_ms, 4),
+        "avg_launch_ms": round(kernel_ms[2] / launches, 3), "frames_per_launch": batch,
+        "note": "achieved = SURVEY §8(d) algorithmic bytes per frame / (engine busy time / frames); busy time = "
+                "union of the k_engine launch intervals (HIP events on the launch streams; two launches overlap, "
+                "avg_launch_ms is the per-launch duration rocprofv3 --stats reports)",
+    }
+    roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 6)
     pmc_path = a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-        k = pmc.get("per_frame_hbm_bytes", {}).get(roof["kernel"])
+        k = pmc.get("per_frame_hbm_bytes", {}).get("engine")
         if k is not None:
             roof["traffic"] = k
             roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         ws = pmc.get("engine_wave_states")
-        if ws and roof["kernel"] == "engine":
+        if ws:
             # SQ counters of the same workload: where the engine's wave time goes
             # (the kernel is dependency-latency-bound, not HBM-bound)
             roof["wave_states"] = {k2: round(ws[k2], 3) for k2 in
                                    ("waiting_frac", "issue_stalled_frac", "issuing_frac", "valu_issue_frac_of_chip")
                                    if k2 in ws}
+    ops_path = os.path.join(ROOT, "profiles", "algorithmic_ops.json")
+    valu = None
+    if os.path.exists(ops_path):
+        ops = json.load(open(ops_path)).get(a.config)
+        if ops:
+            per_frame = ops["pixel_ops_per_p_frame"]
+            ach = per_frame / (engine_busy_ms * 1e-3)
+            valu = {"bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(VALU_PEAK_PIXEL_OPS / 1e12, 1),
+                    "unit": "Tpixel-ops/s", "frac": round(ach / VALU_PEAK_PIXEL_OPS, 5),
+                    "pixel_ops_per_frame": per_frame, "source": "profiles/algorithmic_ops.json",
+                    "note": "SURVEY §8(d) pixel-ops (256 per SAD, 384 per MAD and per lerp, counted by the oracle "
+                            "on band4) / engine busy time; peak = packed 16-bit VALU rate (2 pixel-ops per lane)"}
 
-    # end-to-end: hot path + host entropy on worker threads (rank 0 reports)
     e2e = None
+    e2e_records = {}
     if not a.no_end_to_end:
         ctx2 = cairo_amd.Context(w, h, ring, device=local)
-        if a.batch:
-            ctx2.set_batch(a.batch)
-        e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, barrier, dist, dev, world)
+        ctx2.set_batch(batch)
+        e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, warm_frames, timed_frames, barrier, dist,
+                         dev, world, n_check, e2e_records)
         ctx2.close()
+    ctx.close()
+    del frames
+    torch.cuda.empty_cache()
+
+    api = None
+    if rank == 0 and world == 1 and not a.no_api:
+        api = api_encode(w, h, ring, q, 2 + max(4, min(12, int(100e6 / (w * h)))))
 
     result = {
         "metric": "encoded Mpixels/s (p-frame, q=16) at 1/2/4/8 MI355X; bit-exact vs ref",
@@ -210,58 +312,65 @@ def main():
         "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        "vs_baseline": round(value / REF_CPU_MPIX[a.config], 1) if a.config in REF_CPU_MPIX else None,
+        "vs_baseline_note": "value / BASELINE.md's reference CPU encode (one Xeon core, measured in the survey; "
+                            "the reference publishes no number)",
         "dtype": "int16",
-        "data": "synthetic (band4 generator, seed 1234; SURVEY.md §8(d))",
-        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}])",
-                   "width": w, "height": h, "ring": ring, "quality": q,
+        "data": "synthetic (band4 generator, seed 1234; SURVEY.md §8(d)), resident in HBM",
+        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}] on one GPU)",
+                   "width": w, "height": h, "ring": ring, "quality": q, "frames_per_step": batch,
+                   "timed_frames": timed_frames, "ms_per_frame": round(elapsed * 1e3 / timed_frames, 4),
                    "parallelism": f"replicas: {world} independent stream(s), one per GPU"},
         "roofline": roof,
-        "kernels_avg_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+        "roofline_valu": valu,
         "end_to_end": e2e,
+        "api_encode": api,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        nf = a.cpu_frames or max(2, min(48, int(60e6 / (w * h))))
-        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, nf)
+    if check:
+        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, n_check - 1,
+                                                                   hot_records, e2e_records)
     else:
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
-def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, world):
+def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier, dist, dev, world, n_check,
+               records):
     """Hot path + host entropy through the native frame pipeline
     (cairo_stream_*: entropy on a pool of C++ worker threads); every frame's
     payload is appended to one output buffer (bitstream produced)."""
-    stages = ctx.L.cairo_ctx_stages(ctx.h)
+    stages = ctx.stages
     if a.entropy_threads <= 0:
-        a.entropy_threads = max(1, min(14, (os.cpu_count() or 4) // world - 2))
+        a.entropy_threads = max(1, min(14, host_cpus() // world - 2))
     st = cairo_amd.Stream(ctx, threads=a.entropy_threads)
     out = np.zeros(max(w * h * 4, 1 << 20), np.uint8)  # payload bits of the frames in flight, reused
-
     tl = []
 
-    def collect(tk):
-        st.collect(tk, out, 0)
+    def collect(f, tk):
+        if f < n_check:
+            data, nbits = st.collect(tk)
+            records[f] = record(cairo_amd, w, h, ring, q, f, data, nbits)
+        else:
+            st.collect(tk, out, 0)
         tl.append(st.timeline(tk))
 
     def run(first, count):
         inflight = deque()
         for f in range(first, first + count):
             if len(inflight) == stages:
-                collect(inflight.popleft())
-            inflight.append(st.submit(frame_ptr(f), f, f > 0, q, on_device=True))
+                collect(*inflight.popleft())
+            inflight.append((f, st.submit(frame_ptr(f), f, f > 0, q, on_device=True)))
         while inflight:
-            collect(inflight.popleft())
+            collect(*inflight.popleft())
 
-    run(0, a.warmup)  # I + P warmup
+    run(0, warm)  # I + P warmup
     barrier()
     t0 = time.perf_counter()
     tl.clear()
-    run(a.warmup, a.steps)
+    run(warm, timed)
     barrier()
     el = time.perf_counter() - t0
     st.close()
@@ -273,23 +382,46 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, barrier, dist, dev, 
         "entropy_ms_per_frame_per_thread": round(float(np.mean(T[:, 3] - T[:, 2])) / 1e3, 3),
         "steady_period_ms_per_frame": round(float(np.mean(np.diff(mid[:, 4]))) / 1e3, 4),
     }
-    return {"value": round(aggregate_mpix(w, h, a.steps, world, el), 3), "unit": "Mpix/s",
-            "ms_per_step": round(el * 1e3 / a.steps, 4), "entropy_threads": a.entropy_threads,
+    return {"value": round(aggregate_mpix(w, h, timed, world, el), 3), "unit": "Mpix/s",
+            "ms_per_frame": round(el * 1e3 / timed, 4), "entropy_threads": a.entropy_threads,
             "staging_slots": stages, "pipeline": pipeline,
             "note": "hot path + host entropy (native frame pipeline, cairo_stream_*); payload bits produced"}
 
 
-def cpu_baseline(cairo_amd, w, h, ring, q, pframes):
+def api_encode(w, h, ring, q, frames):
+    """evx1_encoder::encode() timed by a C++ caller built against
+    include/evx1.h (cairo_amd/_lib/evx1_api_caller): one synchronous call per
+    frame, host RGB in, the stream appended to a bit_stream -- the
+    reference's interface (evx1enc.cpp:92-156), PCIe and host entropy
+    included."""
+    if not os.path.exists(API_BIN):
+        return {"error": f"{os.path.relpath(API_BIN, ROOT)} not built"}
+    r = subprocess.run([API_BIN, str(w), str(h), str(ring), str(q), str(frames)], capture_output=True, text=True,
+                       timeout=300)
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}: {r.stderr[-400:]}"}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    ms = d["encode_ms"][1:]  # P-frames
+    return {"value": round(w * h * len(ms) / (sum(ms) * 1e-3) / 1e6, 3), "unit": "Mpix/s",
+            "ms_per_p_frame": round(float(np.mean(ms)), 3), "ms_i_frame": round(d["encode_ms"][0], 3),
+            "fps": round(1e3 / float(np.mean(ms)), 2), "frames": frames, "stream_fnv1a64": d["fnv1a64"],
+            "note": "synchronous evx1_encoder::encode() per frame (drop-in C++ API, vtable call, host RGB, "
+                    "host entropy on the calling thread)"}
+
+
+def cpu_baseline(cairo_amd, w, h, ring, q, pframes, hot_records, e2e_records):
     """The oracle (plain-C restatement of the reference encoder, test
     infrastructure) on one host core over a bounded sample: frame 0 (I) +
-    `pframes` P-frames; P-frame Mpix/s.  The same frames are then encoded by
-    the GPU path + host entropy and compared bit for bit (the checker role)."""
+    `pframes` P-frames; P-frame Mpix/s.  The GPU records of the same frames,
+    taken from the timed hot-path context and from the end-to-end pipeline,
+    are then compared bit for bit (the checker role)."""
     from oracle import oracle as orc
 
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
     ref = []
     tp = 0.0
+    orc.op_counts(reset=True)
     for t in range(pframes + 1):
         rgb = cairo_amd.make_band4(w, h, t)
         t0 = time.perf_counter()
@@ -300,25 +432,24 @@ def cpu_baseline(cairo_amd, w, h, ring, q, pframes):
         ref.append(orc.canonical_frame_bytes(data, n, t == 0))
     base = {"value": round(w * h * pframes / tp / 1e6, 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
             "sample": f"{w}x{h} q={q} R={ring}: frame 0 (I, untimed) + {pframes} P-frames timed, band4 seed 1234, "
-                      f"oracle/evx_oracle.c -O2, one thread"}
-    try:
-        import platform
+                      f"oracle/evx_oracle.c -O2, one thread",
+            "cpu": cpu_model(), "host_cpus_available": host_cpus()}
 
-        base["cpu"] = platform.processor() or open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": ")
-    except Exception:
-        pass
-    # bit-exact check of the GPU path on the same frames (drop-in encoder API)
-    enc = cairo_amd.Encoder(ring=ring)
-    enc.set_quality(q)
-    bs = cairo_amd.BitStream(w * h * 64)
-    mism = []
-    for t in range(pframes + 1):
-        bs.empty()
-        enc.encode(cairo_amd.make_band4(w, h, t), bs)
-        if orc.canonical_frame_bytes(bs.data(), bs.bits(), t == 0) != ref[t]:
-            mism.append(t)
-    enc.close()
-    exact = {"frames_checked": pframes + 1, "mismatched_frames": mism, "bit_exact": not mism}
+    def compare(recs):
+        mism = [t for t in range(pframes + 1)
+                if t not in recs or orc.canonical_frame_bytes(recs[t][0], recs[t][1], t == 0) != ref[t]]
+        return {"frames_checked": pframes + 1, "mismatched_frames": mism}
+
+    hot = compare(hot_records)
+    exact = {"hot_path_context": hot,
+             "what": "frames 0..n of the timed context (same batch, overlapping launches) serialized on the host, "
+                     "and of the end-to-end pipeline, vs the oracle's stream records (header byte 7 and tail bits "
+                     "masked)"}
+    ok = not hot["mismatched_frames"]
+    if e2e_records:
+        exact["end_to_end_pipeline"] = compare(e2e_records)
+        ok = ok and not exact["end_to_end_pipeline"]["mismatched_frames"]
+    exact["bit_exact"] = ok
     return base, exact
 
 

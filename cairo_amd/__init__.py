@@ -36,6 +36,9 @@ BLOCK_DESC = np.dtype(
 assert BLOCK_DESC.itemsize == 16
 
 EVX_SUCCESS = 0
+# EVX_PEEK_STATE (reference evx1.h:55-64)
+PEEK_SOURCE, PEEK_PREDICTION, PEEK_BLOCK_TABLE, PEEK_QUANT_TABLE, PEEK_SPMP_TABLE, PEEK_BLOCK_VARIANCE, \
+    PEEK_DESTINATION = range(7)
 MAX_BATCH = 32  # kMaxBatch (kernels.h): frames per engine launch, stamp layout
 EVX_ERROR_HARDWAREFAIL = 5
 
@@ -62,6 +65,7 @@ def lib() -> ctypes.CDLL:
     P, I, U, V = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, None
     sig = {
         "cairo_ctx_create": (I, [U, U, U, I, ctypes.POINTER(P)]),
+        "cairo_ctx_create_ex": (I, [U, U, U, I, I, ctypes.POINTER(P)]),
         "cairo_ctx_destroy": (I, [P]),
         "cairo_ctx_reset": (I, [P]),
         "cairo_ctx_submit": (I, [P, P, I, U, U, U, ctypes.POINTER(I)]),
@@ -88,6 +92,7 @@ def lib() -> ctypes.CDLL:
         "cairo_stream_collect": (I, [P, I, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
         "cairo_stream_destroy": (I, [P]),
         "cairo_stream_timeline": (I, [P, I, P]),
+        "cairo_stream_payload_bits": (I, [P, I, ctypes.POINTER(ctypes.c_uint64)]),
         "cairo_bits_append": (I, [P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), P, ctypes.c_uint64]),
         "evx_encoder_create": (I, [ctypes.POINTER(P)]),
         "evx_encoder_destroy": (I, [P]),
@@ -96,6 +101,7 @@ def lib() -> ctypes.CDLL:
         "evx_encoder_set_quality": (I, [P, ctypes.c_uint8]),
         "evx_encoder_encode": (I, [P, P, U, U, P]),
         "evx_encoder_set_ring": (I, [P, U]),
+        "evx_encoder_peek": (I, [P, I, P]),
         "evx_encoder_set_device": (I, [P, I]),
         "evx_bitstream_create": (P, [U]),
         "evx_bitstream_destroy": (V, [P]),
@@ -129,6 +135,18 @@ def _ck(status: int, what: str) -> None:
 def _ptr(a: np.ndarray) -> int:
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data
+
+
+def _host_frame(rgb, width: int, height: int) -> int:
+    """Address of a host RGB888 frame, after checking that it holds a whole
+    width x height frame (the native side copies width*height*3 bytes from
+    it asynchronously)."""
+    if not isinstance(rgb, np.ndarray):
+        raise TypeError("host frames are numpy arrays (pass on_device=True for a device address)")
+    if rgb.dtype != np.uint8 or rgb.shape != (height, width, 3) or not rgb.flags["C_CONTIGUOUS"]:
+        raise ValueError(f"frame must be a C-contiguous uint8 array of shape ({height}, {width}, 3), "
+                         f"got {rgb.dtype} {rgb.shape}")
+    return rgb.ctypes.data
 
 
 def make_band4(w: int, h: int, t: int, seed: int = 1234) -> np.ndarray:
@@ -172,13 +190,13 @@ def _view(addr: int, dtype, count: int) -> np.ndarray:
 class Context:
     """The encode-path backend (``cairo_ctx_*``): one encoder's device state."""
 
-    def __init__(self, width: int, height: int, ring: int = 4, device: int = 0):
+    def __init__(self, width: int, height: int, ring: int = 4, device: int = 0, stages: int = 64):
         self.L = lib()
         self.width, self.height, self.ring, self.device = width, height, ring, device
         self.wa, self.ha = (width + 15) & ~15, (height + 15) & ~15
         self.wmb, self.hmb = self.wa // 16, self.ha // 16
         p = ctypes.c_void_p()
-        _ck(self.L.cairo_ctx_create(width, height, ring, device, ctypes.byref(p)), "cairo_ctx_create")
+        _ck(self.L.cairo_ctx_create_ex(width, height, ring, device, stages, ctypes.byref(p)), "cairo_ctx_create")
         self.h = p
         self._keep = {}  # ticket -> host RGB frame still being copied
 
@@ -193,9 +211,13 @@ class Context:
         except Exception:
             pass
 
+    @property
+    def stages(self) -> int:
+        return int(self.L.cairo_ctx_stages(self.h))
+
     def submit(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> int:
         t = ctypes.c_int()
-        ptr = rgb if on_device else _ptr(rgb)
+        ptr = rgb if on_device else _host_frame(rgb, self.width, self.height)
         _ck(
             self.L.cairo_ctx_submit(self.h, ptr, int(on_device), index, int(inter), quality, ctypes.byref(t)),
             "cairo_ctx_submit",
@@ -283,7 +305,9 @@ class Context:
         _ck(self.L.cairo_ctx_set_profiling(self.h, int(enable)), "set_profiling")
 
     def take_timings(self):
-        ms = (ctypes.c_double * 3)()
+        """-> ([convert ms, 0, engine ms summed over launches, engine busy ms
+        (union of the launch intervals)], frames) since the last call."""
+        ms = (ctypes.c_double * 4)()
         n = ctypes.c_int()
         _ck(self.L.cairo_ctx_take_timings(self.h, ms, ctypes.byref(n)), "take_timings")
         return list(ms), n.value
@@ -354,7 +378,7 @@ class Stream:
 
     def submit(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> int:
         t = ctypes.c_int()
-        ptr = rgb if on_device else _ptr(rgb)
+        ptr = rgb if on_device else _host_frame(rgb, self.ctx.width, self.ctx.height)
         _ck(self.L.cairo_stream_submit(self.h, ptr, int(on_device), index, int(inter), quality, ctypes.byref(t)),
             "cairo_stream_submit")
         if not on_device:
@@ -366,8 +390,9 @@ class Stream:
         None, return (bytes, nbits) of the payload alone."""
         if out is None:
             p = ctypes.c_uint64(0)
-            # size query is not separate: collect into a buffer large enough for any frame
-            buf = np.zeros(self.ctx.wa * self.ctx.ha * 8 + 65536, np.uint8)
+            _ck(self.L.cairo_stream_payload_bits(self.h, ticket, ctypes.byref(p)), "cairo_stream_payload_bits")
+            buf = np.zeros(p.value // 8 + 8, np.uint8)
+            p = ctypes.c_uint64(0)
             _ck(self.L.cairo_stream_collect(self.h, ticket, _ptr(buf), buf.size, ctypes.byref(p)),
                 "cairo_stream_collect")
             self._keep.pop(ticket, None)
@@ -454,8 +479,19 @@ class Encoder:
         _ck(self.L.evx_encoder_clear(self.h), "clear")
 
     def encode(self, rgb: np.ndarray, bs: BitStream) -> None:
+        if rgb.ndim != 3 or rgb.shape[2] != 3:
+            raise ValueError(f"frame must have shape (height, width, 3), got {rgb.shape}")
         h, w = rgb.shape[:2]
-        _ck(self.L.evx_encoder_encode(self.h, _ptr(np.ascontiguousarray(rgb)), w, h, bs.h), "encode")
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8) if rgb.dtype == np.uint8 else None
+        if rgb is None:
+            raise ValueError("frame must be uint8 RGB888")
+        _ck(self.L.evx_encoder_encode(self.h, _ptr(rgb), w, h, bs.h), "encode")
+
+    def peek(self, state: int, width: int, height: int) -> np.ndarray:
+        """Debug view of the last encoded frame (EVX_PEEK_*, evx1.h) -> RGB (h, w, 3)."""
+        out = np.zeros((height, width, 3), np.uint8)
+        _ck(self.L.evx_encoder_peek(self.h, state, _ptr(out)), "peek")
+        return out
 
     def close(self) -> None:
         if self.h:

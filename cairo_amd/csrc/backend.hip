@@ -2,13 +2,14 @@
 //
 // One context = one encoder's device state in HBM (DESIGN.md "Data layout"):
 //   ring          R contiguous plane sets (reconstruction slots, frame n -> n % R)
-//   16 staging slots, one per frame in flight, each with its own
+//   staging slots (64 for pipelined callers, 2 for the synchronous drop-in
+//     encoder/decoder), one per frame in flight, each with its own
 //     source planes (convert output), output_cache planes (coefficients),
 //     block table, inter-search records, granules, RGB staging and pinned
 //     host buffers for the table + coefficients
 //   sync          batch flags (zeroed per launch)
-// Frames are submitted into a batch (up to batch_max, default 8) that is
-// launched when full or when a caller waits on one of its frames:
+// Frames are submitted into a batch (up to batch_max, cairo_default_batch)
+// that is launched when full or when a caller waits on one of its frames:
 //   memset(sync) -> convert (all frames) -> engine (inter search, row coding,
 //   deblock, pipelined across the frames)
 // and on the copy stream, after the engine: D2H of each frame's table and
@@ -16,6 +17,7 @@
 // while the GPU runs the next batch).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -33,7 +35,9 @@ using namespace cairo;
 
 namespace {
 
-constexpr int kStages = 64;      // staging slots (frames in flight): two 32-frame or four 16-frame batches
+constexpr int kDefaultStages = 64;  // staging slots (frames in flight): two 32-frame or four 16-frame batches
+constexpr int kMaxStages = 256;
+constexpr int kLaunchSlots = 64;    // per-launch host records (frame views, timing events), reused round-robin
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
 // Frames per launch by default, from measured sweeps (tools/batch_sweep.sh):
 // 32 for frames up to 720p (launch boundaries cost a visible share there),
@@ -44,7 +48,6 @@ inline int default_batch(size_t mbs) {
   return mbs <= (size_t)kSmallFrameMBs ? 32 : mbs <= (size_t)kMidFrameMBs ? 12 : 16;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
-constexpr int kMaxLaunchWG = 384;  // workgroups per launch: two launches fill the 768 slots (3 per CU)
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)
               kInvalidResource = 8;
 
@@ -64,6 +67,24 @@ struct TimedBatch {
   int frames = 0;
   bool pending = false;
 };
+
+// Length of the union of [start, end) intervals (ms): the time the engine
+// was running at all, with the two in-flight launches overlapping.
+double union_length(std::vector<std::pair<double, double>>& iv) {
+  std::sort(iv.begin(), iv.end());
+  double total = 0, s = 0, e = -1e300;
+  for (const auto& p : iv) {
+    if (p.first > e) {
+      if (e > s) total += e - s;
+      s = p.first;
+      e = p.second;
+    } else if (p.second > e) {
+      e = p.second;
+    }
+  }
+  if (e > s) total += e - s;
+  return total;
+}
 
 }  // namespace
 
@@ -87,13 +108,14 @@ struct cairo_ctx {
   int16_t* ring_buf = nullptr;
   int32_t *sync = nullptr, *sticky = nullptr;
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
-  FrameArgs* fdesc_host = nullptr;  // pinned [kStages][kMaxBatch]: per-frame views per launch
+  FrameArgs* fdesc_host = nullptr;  // pinned [kLaunchSlots][kMaxBatch]: per-frame views per launch
   FrameArgs* fdesc = nullptr;       // device copy
   int fdesc_next = 0;
   int32_t* trace_host = nullptr;  // diagnostic live trace (mapped), opt-in via set_debug(4)
   int32_t* trace_dev = nullptr;
   size_t sync_words = 0;
-  Stage st[kStages];
+  int stages = kDefaultStages;
+  std::vector<Stage> st;  // [stages]
   int next_ticket = 0;
   uint32_t epoch = 0;
   int batch_max = 16;
@@ -101,11 +123,14 @@ struct cairo_ctx {
   int npend = 0;
   int last_slot = -1;  // slot of the last launched frame
   int wg_rows = 0;
+  int max_rows = 0;  // row coders (= helpers) per launch that stay co-resident with the other in-flight launch
   bool profiling = false;
-  TimedBatch tb[kStages];
+  TimedBatch tb[kLaunchSlots];
   int tb_next = 0;
   double acc_ms[kTimed] = {0, 0, 0};
   int acc_frames = 0;
+  hipEvent_t t_base = nullptr;  // profiling epoch: engine intervals are measured from it
+  std::vector<std::pair<double, double>> busy;  // engine [start, end) per launch, ms after t_base
   int16_t* predeblock = nullptr;  // debug: pre-deblock reconstruction of the last frame (opt-in)
   uint64_t* stamps = nullptr;     // diagnostic phase stamps (opt-in)
   // Thread safety (the frame pipeline of pipeline.cpp calls in from its
@@ -179,6 +204,7 @@ void free_ctx(cairo_ctx* c) {
     for (auto& e : t.ev)
       if (e) (void)hipEventDestroy(e);
   if (c->engine_done) (void)hipEventDestroy(c->engine_done);
+  if (c->t_base) (void)hipEventDestroy(c->t_base);
   for (auto& ev : c->batch_end)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->area_ready)
@@ -195,16 +221,25 @@ void free_ctx(cairo_ctx* c) {
   delete c;
 }
 
+// Fresh-encoder state (every stream idle): zero planes, tables and granules,
+// the launch sync areas and the sticky timeout word, so a context that once
+// reported a timed-out wait is usable again after cairo_ctx_reset.
 int zero_state(cairo_ctx* c) {
-  CK(hipMemsetAsync(c->src, 0, c->plane_elems * 2 * kStages, c->ks));
-  CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2 * kStages, c->ks));
+  const size_t S = (size_t)c->stages;
+  CK(hipMemsetAsync(c->src, 0, c->plane_elems * 2 * S, c->ks));
+  CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2 * S, c->ks));
   CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
-  CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * kStages, c->ks));
+  CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * S, c->ks));
   // granule tags start at 0; the n-th submission after a reset publishes tag n
-  CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * kStages, c->ks));
+  CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * S, c->ks));
+  CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t) * kSyncAreas, c->ks));
+  CK(hipMemsetAsync(c->sticky, 0, sizeof(int32_t), c->ks));
   CK(hipStreamSynchronize(c->ks));
   c->epoch = 0;
   c->last_slot = -1;
+  c->batches = 0;  // the first launch after a reset depends on no earlier launch
+  c->prev_nframes = 0;
+  for (auto& s : c->st) *s.err = 0;
   return kSuccess;
 }
 
@@ -216,6 +251,10 @@ int collect_times(cairo_ctx* c, TimedBatch& t) {
     CK(hipEventElapsedTime(&ms, t.ev[k], t.ev[k + 1]));
     c->acc_ms[k] += ms;
   }
+  float s0 = 0, s1 = 0;  // the engine's interval on the common clock
+  CK(hipEventElapsedTime(&s0, c->t_base, t.ev[2]));
+  CK(hipEventElapsedTime(&s1, c->t_base, t.ev[3]));
+  c->busy.emplace_back((double)s0, (double)s1);
   c->acc_frames += t.frames;
   t.pending = false;
   return kSuccess;
@@ -231,7 +270,7 @@ int flush(cairo_ctx* c) {
   // frame descriptors -> device (a ring of pinned slots: the copy of an earlier
   // launch may still be pending when this one is written)
   const int fslot = c->fdesc_next;
-  c->fdesc_next = (c->fdesc_next + 1) % kStages;
+  c->fdesc_next = (c->fdesc_next + 1) % kLaunchSlots;
   FrameArgs* fh = c->fdesc_host + (size_t)fslot * kMaxBatch;
   FrameArgs* fd = c->fdesc + (size_t)fslot * kMaxBatch;
   bool any_inter = false;
@@ -243,10 +282,11 @@ int flush(cairo_ctx* c) {
   (void)any_inter;
   // Launch b alternates streams and sync areas; it follows launch b-1, which
   // may still be running: its frame 0 reads the deblock progress of b-1's last
-  // frame.  Residency: 2 workgroups per CU (VGPRs) x 256 CUs = 512; a launch
-  // takes at most 240 so that two launches are always co-resident.  Every row
-  // has a coder and a helper (inter search + deblock) living as long as the
-  // row: equal pools.
+  // frame.  Residency: a launch takes at most half of the engine's resident
+  // workgroup slots (CUs x occupancy, measured at create: 256 x 3 = 768 on a
+  // full MI355X), so two launches are always co-resident.  Every row has a
+  // coder and a helper (inter search + deblock) living as long as the row:
+  // equal pools.
   const long long b = c->batches++;
   hipStream_t st = (b & 1) ? c->ks2 : c->ks;
   const int area = (int)(b % kSyncAreas);
@@ -257,7 +297,7 @@ int flush(cairo_ctx* c) {
             : nullptr;
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
   c->prev_nframes = e.nframes;
-  e.n_rows = c->wg_rows > 0 ? c->wg_rows : kMaxLaunchWG / 2;
+  e.n_rows = c->wg_rows > 0 ? std::min(c->wg_rows, c->max_rows) : c->max_rows;
   if (e.n_rows > rows) e.n_rows = rows;
   e.n_helpers = e.n_rows;
   // this sync area was last used by launch b-3 and read by launch b-2
@@ -269,7 +309,7 @@ int flush(cairo_ctx* c) {
   TimedBatch* tb = nullptr;
   if (c->profiling) {
     tb = &c->tb[c->tb_next];
-    c->tb_next = (c->tb_next + 1) % kStages;
+    c->tb_next = (c->tb_next + 1) % kLaunchSlots;
     int r = collect_times(c, *tb);  // its events are about to be reused
     if (r) return r;
   }
@@ -342,10 +382,16 @@ int sync_all(cairo_ctx* c) {
 extern "C" {
 
 int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device, cairo_ctx** out) {
+  return cairo_ctx_create_ex(width, height, ring, device, kDefaultStages, out);
+}
+
+int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int device, int stages,
+                        cairo_ctx** out) {
   // The reference indexes blocks with uint16 (deblock.cpp, serialize.cpp): at
   // most 65535 macroblocks per frame.
   if (!out || width == 0 || height == 0 || (width & 1) || (height & 1) || ring < 1 ||
-      ring > (uint32_t)kMaxRing || ((width + 15) / 16) * ((height + 15) / 16) > 65535u)
+      ring > (uint32_t)kMaxRing || ((width + 15) / 16) * ((height + 15) / 16) > 65535u || stages < 2 ||
+      stages > kMaxStages)
     return kInvalidArg;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
@@ -364,7 +410,9 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   c->ring = ring;
   c->plane_elems = (size_t)c->wa * c->ha * 3 / 2;
   c->mbs = (size_t)c->wmb * c->hmb;
-  c->batch_max = default_batch(c->mbs);
+  c->stages = stages;
+  c->st.resize((size_t)stages);
+  c->batch_max = std::min(default_batch(c->mbs), stages / 2);
   c->nref = ring > 1 ? ring - 1 : 1;
   c->sync_words = (size_t)SyncLayout::words((int)c->hmb, (int)(c->wmb + 3) / 4);
   int r = kSuccess;
@@ -377,17 +425,25 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
     }                                  \
   } while (0)
   TRY(hipSetDevice(device));
+  {  // engine pools per launch: half of the resident workgroup slots, halved
+     // again between helpers and row coders
+    int cus = 0, per_cu = 0;
+    TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    TRY(engine_blocks_per_cu(&per_cu));
+    c->max_rows = std::max(1, cus * per_cu / 4);
+  }
   TRY(hipStreamCreateWithFlags(&c->ks, hipStreamNonBlocking));
   TRY(hipStreamCreateWithFlags(&c->ks2, hipStreamNonBlocking));
   TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
-  TRY(hipMalloc(&c->src, c->plane_elems * 2 * kStages));
-  TRY(hipMalloc(&c->coef, c->plane_elems * 2 * kStages));
+  const size_t S = (size_t)stages;
+  TRY(hipMalloc(&c->src, c->plane_elems * 2 * S));
+  TRY(hipMalloc(&c->coef, c->plane_elems * 2 * S));
   TRY(hipMalloc(&c->ring_buf, c->plane_elems * 2 * ring));
-  TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * kStages));
-  TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * kStages));
-  TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * kStages));
-  TRY(hipMalloc(&c->gran, c->mbs * kGranuleStride * sizeof(uint64_t) * kStages));
-  TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * kStages));
+  TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * S));
+  TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * S));
+  TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * S));
+  TRY(hipMalloc(&c->gran, c->mbs * kGranuleStride * sizeof(uint64_t) * S));
+  TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * S));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t) * kSyncAreas));
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
@@ -403,8 +459,8 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
           if (r >= 0 && r < hmb) o[n++] = (f << 16) | r;
         }
     }
-    TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kStages * kMaxBatch, hipHostMallocDefault));
-    TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kStages * kMaxBatch));
+    TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch, hipHostMallocDefault));
+    TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch));
     TRY(hipMalloc(&c->order, ord.size() * sizeof(int32_t)));
     TRY(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
@@ -417,6 +473,7 @@ int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
   for (auto& t : c->tb)
     for (auto& e : t.ev) TRY(hipEventCreate(&e));
   TRY(hipEventCreateWithFlags(&c->engine_done, hipEventDisableTiming));
+  TRY(hipEventCreate(&c->t_base));
   for (auto& ev : c->batch_end) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : c->area_ready) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 #undef TRY
@@ -445,7 +502,7 @@ int cairo_ctx_reset(cairo_ctx* c) {
   return zero_state(c);
 }
 
-int cairo_ctx_stages(const cairo_ctx*) { return kStages; }
+int cairo_ctx_stages(const cairo_ctx* c) { return c ? c->stages : 0; }
 
 int cairo_default_batch(uint32_t width, uint32_t height) {
   if (!width || !height) return 0;
@@ -453,7 +510,7 @@ int cairo_default_batch(uint32_t width, uint32_t height) {
 }
 
 int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
-  if (!c || frames < 1 || frames > kMaxBatch || frames > kStages / 2) return kInvalidArg;
+  if (!c || frames < 1 || frames > kMaxBatch || frames > c->stages / 2) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   int r = flush(c);
   if (r) return r;
@@ -462,7 +519,9 @@ int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
 }
 
 int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
-  if (!c || rows < 0) return kInvalidArg;
+  // more row coders than stay co-resident with the other in-flight launch
+  // would leave tasks to workgroups that never get a slot
+  if (!c || rows < 0 || rows > c->max_rows) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   c->wg_rows = rows;
   return kSuccess;
@@ -471,11 +530,17 @@ int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
 int cairo_ctx_set_profiling(cairo_ctx* c, int enable) {
   if (!c) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
+  CK(hipSetDevice(c->device));
+  if (enable && !c->profiling) {
+    int r = flush(c);
+    if (r) return r;
+    CK(hipEventRecord(c->t_base, c->ks));
+  }
   c->profiling = enable != 0;
   return kSuccess;
 }
 
-int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
+int cairo_ctx_take_timings(cairo_ctx* c, double ms[4], int* frames) {
   if (!c) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
@@ -489,6 +554,8 @@ int cairo_ctx_take_timings(cairo_ctx* c, double ms[3], int* frames) {
     if (ms) ms[k] = c->acc_ms[k];
     c->acc_ms[k] = 0;
   }
+  if (ms) ms[kTimed] = union_length(c->busy);
+  c->busy.clear();
   if (frames) *frames = c->acc_frames;
   c->acc_frames = 0;
   return kSuccess;
@@ -500,7 +567,7 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   const int t = c->next_ticket;
-  const int slot = t % kStages;
+  const int slot = t % c->stages;
   Stage& s = c->st[slot];
   if (s.busy) {
     fprintf(stderr, "[cairo_amd] staging slot of ticket %d not released\n", s.ticket);
@@ -519,7 +586,7 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   f.quality = (int)quality;
   f.epoch = ++c->epoch;
   f.slot = slot;
-  f.prev_slot = (t + kStages - 1) % kStages;
+  f.prev_slot = (t + c->stages - 1) % c->stages;
   f.decode = 0;  // decode_frame never leaves a decode frame pending
   f.host_table = nullptr;
   f.host_coef = nullptr;
@@ -573,7 +640,7 @@ static int frame_result(cairo_ctx* c, Stage& s, cairo_frame_result* out, bool po
 
 int cairo_ctx_wait(cairo_ctx* c, int ticket, cairo_frame_result* out) {
   if (!c || !out || ticket < 0) return kInvalidArg;
-  Stage& s = c->st[ticket % kStages];
+  Stage& s = c->st[ticket % c->stages];
   {
     std::lock_guard<std::mutex> lk(c->mu);
     if (!s.busy || s.ticket != ticket) return kInvalidResource;
@@ -593,7 +660,7 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
   CK(hipSetDevice(c->device));
   int r = flush(c);  // encode frames still pending go first, in their own launch
   if (r) return r;
-  const int t = c->next_ticket, slot = t % kStages;
+  const int t = c->next_ticket, slot = t % c->stages;
   Stage& s = c->st[slot];
   if (s.busy) {
     fprintf(stderr, "[cairo_amd] staging slot of ticket %d not released\n", s.ticket);
@@ -606,7 +673,7 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
   f.quality = 1;
   f.epoch = ++c->epoch;
   f.slot = slot;
-  f.prev_slot = (t + kStages - 1) % kStages;
+  f.prev_slot = (t + c->stages - 1) % c->stages;
   f.decode = 1;
   f.host_table = reinterpret_cast<const BlockDesc*>(table);
   f.host_coef = coef;
@@ -642,7 +709,7 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
 int cairo_ctx_release(cairo_ctx* c, int ticket) {
   if (!c || ticket < 0) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
-  Stage& s = c->st[ticket % kStages];
+  Stage& s = c->st[ticket % c->stages];
   if (s.ticket != ticket) return kInvalidResource;
   s.busy = false;
   return kSuccess;
@@ -699,6 +766,10 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
     CK(hipHostMalloc(&c->trace_host, 4096 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
     memset(c->trace_host, 0xFF, 4096 * sizeof(int32_t));
     CK(hipHostGetDevicePointer((void**)&c->trace_dev, c->trace_host, 0));
+  }
+  if (flags & 8) {
+    const int32_t one = 1;
+    CK(hipMemcpy(c->sticky, &one, sizeof(one), hipMemcpyHostToDevice));
   }
   return kSuccess;
 }
@@ -796,7 +867,7 @@ namespace cairo {
 int ctx_wait_launched(cairo_ctx* c, int ticket, const std::atomic<bool>* stop,
                       cairo_frame_result* out) {
   if (!c || !out || ticket < 0) return kInvalidArg;
-  Stage& s = c->st[ticket % kStages];
+  Stage& s = c->st[ticket % c->stages];
   {
     std::unique_lock<std::mutex> lk(c->mu);
     if (!s.busy || s.ticket != ticket) return kInvalidResource;
@@ -810,7 +881,7 @@ int ctx_flush(cairo_ctx* c, int ticket) {
   if (!c) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   if (ticket >= 0) {  // only if that frame is still in the pending batch
-    const Stage& s = c->st[ticket % kStages];
+    const Stage& s = c->st[ticket % c->stages];
     if (!s.busy || s.ticket != ticket || s.launched) return kSuccess;
   }
   CK(hipSetDevice(c->device));

@@ -104,7 +104,7 @@ class gpu_decoder : public evx1_decoder {
     ha_ = (height_ + 15) & ~15u;
     wmb_ = wa_ / 16;
     hmb_ = ha_ / 16;
-    if (cairo_ctx_create(width_, height_, ring_, device_, &ctx_)) return EVX_ERROR_HARDWAREFAIL;
+    if (cairo_ctx_create_ex(width_, height_, ring_, device_, 2, &ctx_)) return EVX_ERROR_HARDWAREFAIL;  // synchronous: 2 slots
     table_ = (cairo::BlockDesc *)calloc((size_t)wmb_ * hmb_, sizeof(cairo::BlockDesc));
     coef_ = (int16 *)calloc((size_t)wa_ * ha_ * 3 / 2, sizeof(int16));
     if (!table_ || !coef_) {

@@ -189,7 +189,9 @@ class gpu_encoder : public evx1_encoder {
   }
   evx_status initialize(uint32 width, uint32 height) {  // evx1enc.cpp:66-90
     if (width > 0xFFFF || height > 0xFFFF) return EVX_ERROR_INVALIDARG;
-    if (cairo_ctx_create(width, height, ring_, device_, &ctx_)) return EVX_ERROR_HARDWAREFAIL;
+    // one frame in flight: two staging slots (the previous frame's output_cache
+    // stays in the other one, for the copy-macroblock chain)
+    if (cairo_ctx_create_ex(width, height, ring_, device_, 2, &ctx_)) return EVX_ERROR_HARDWAREFAIL;
     const size_t mbs = (size_t)((width + 15) / 16) * ((height + 15) / 16);
     last_table_ = (uint8 *)calloc(mbs, 16);
     if (!last_table_) return EVX_ERROR_OUTOFMEMORY;
@@ -236,6 +238,9 @@ int evx_encoder_insert_intra(void *enc) { return ((evx::evx1_encoder *)enc)->ins
 int evx_encoder_set_quality(void *enc, uint8_t q) { return ((evx::evx1_encoder *)enc)->set_quality(q); }
 int evx_encoder_encode(void *enc, const void *rgb, uint32_t w, uint32_t h, void *bs) {
   return ((evx::evx1_encoder *)enc)->encode((void *)rgb, w, h, (evx::bit_stream *)bs);
+}
+int evx_encoder_peek(void *enc, int state, void *rgb) {
+  return ((evx::evx1_encoder *)enc)->peek((evx::EVX_PEEK_STATE)state, rgb);
 }
 int evx_encoder_set_ring(void *enc, uint32_t ring) {
   return static_cast<evx::gpu_encoder *>((evx::evx1_encoder *)enc)->set_ring(ring);

@@ -138,7 +138,7 @@ struct EngineArgs {
                                        // if it belongs to a launch that may still run (else nullptr)
   int32_t* sticky;
   uint64_t* stamps;
-  int n_helpers, n_rows;   // worker pools (workgroups); blockIdx order: helpers, rows
+  int n_helpers, n_rows;   // worker pools (workgroups, equal sizes), interleaved in blockIdx runs of 8
   int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)
   const int32_t* order;    // [nframes * hmb] task order of every pool: (frame << 16 | row),
                            // sorted by (row + kOrderSlope * frame, frame)
@@ -156,6 +156,8 @@ hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);
 // The pipelined encode engine: inter search, macroblock rows (intra search,
 // classify, transform, quantize, reconstruct) and in-loop deblock.
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s);
+// Engine workgroups resident per CU (occupancy of k_engine: 3 on gfx950).
+hipError_t engine_blocks_per_cu(int* n);
 // Debug: rebuild the pre-deblock reconstruction of frame j of the batch from
 // its granules into plane set dst.
 hipError_t launch_unpack_granules(const EngineArgs& e, int j, PlaneSet dst, hipStream_t s);

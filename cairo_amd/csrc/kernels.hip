@@ -1,11 +1,18 @@
 // cairo_amd/csrc/kernels.hip -- the EVX-1 encode hot path on gfx950 (CDNA4).
 //
-//   K0 k_convert      RGB888 -> planar YUV 4:2:0 int16        convert.cpp:95-160
-//   K1 k_inter_search one wave64 per (macroblock, reference)  motion.cpp:421-494
-//   K2 k_mb_rows      row-worker wavefront: intra search, classify, transform,
-//                     VAQ, quantize, reconstruct              encode.cpp:17-203,
-//                                                             decode.cpp:15-144
-//   K3 k_deblock      band-worker wavefront, in place         deblock.cpp:201-284
+//   k_convert_batch  RGB888 -> planar YUV 4:2:0 int16, every frame of a
+//                    launch                                    convert.cpp:95-160
+//   k_engine         one persistent launch per batch of frames, pipelined
+//                    across frames, two pools of 256-thread workgroups:
+//     row helpers    inter search of their MB row (one wave per MB and
+//                    reference, LDS window)                    motion.cpp:421-494
+//                    + the in-place deblock of the row behind its coder
+//                                                              deblock.cpp:201-284
+//     row coders     intra search, classify, transform, VAQ, quantize,
+//                    reconstruct, left to right                encode.cpp:17-203,
+//                                                              decode.cpp:15-144
+//   k_yuv_to_rgb     the decoder's output conversion          convert.cpp:162-223
+//   k_kat_transform  known-answer entry of the transform chain (tests)
 //
 // All arithmetic is integer and restates the reference bit for bit (see
 // evx_defs.h for the helpers).  Searches evaluate candidates in parallel and
@@ -1845,8 +1852,8 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 
 // ---------------------------------------------------------------------------
 // The engine: one persistent launch encodes a batch of consecutive frames,
-// pipelined across frames.  Two worker pools (blockIdx ranges: helpers, then
-// row coders) dequeue (frame, row) tasks in e.order (by row + slope * frame):
+// pipelined across frames.  Two worker pools (helpers and row coders,
+// interleaved in blockIdx runs of 8: is_helper) dequeue (frame, row) tasks in e.order (by row + slope * frame):
 //   helper (j, r): inter search of row r, group g (MBs 4g..4g+3) once the
 //           previous frame is final on MB rows r-2..r+2 over the group's
 //           search window [64g-32, 64g+96) (this also covers every older
@@ -1865,6 +1872,15 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 
 constexpr int kPrioFrameMBs = 4000;  // helpers get issue priority above this frame size
 
+// Pool of workgroup b out of n (n/2 helpers, n/2 row coders): blocks
+// alternate in runs of 8, one run per XCD in dispatch order, so both pools
+// are spread over every XCD and a launch that is only partly resident (a
+// shared or partitioned GPU) still has workers of both pools.
+__device__ __forceinline__ bool is_helper(int b, int n) {
+  const int full = n & ~15;
+  return b < full ? (b & 15) < 8 : (b - full) < ((n - full) >> 1);
+}
+
 template <bool kDecode>
 __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   __shared__ EngineLds L;
@@ -1874,7 +1890,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   if (ks && threadIdx.x == 0)
     __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int total = e.nframes * hmb;
-  if (b < e.n_helpers) {
+  if (is_helper(b, e.n_helpers + e.n_rows)) {
     // The helpers' inter records gate every row coder at its group starts:
     // on large frames they win the SIMD issue arbitration against the coders'
     // waves (A/B: 1080p +3 %, 4K +3 %; 720p -1 %, so not there).
@@ -1956,6 +1972,10 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   }
   a.rgb = f.rgb;
   return a;
+}
+
+hipError_t engine_blocks_per_cu(int* n) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, reinterpret_cast<const void*>(&k_engine<false>), 256, 0);
 }
 
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s) {

@@ -281,6 +281,9 @@ int cairo_stream_collect(cairo_stream* s, int ticket, uint8_t* out, uint64_t out
       r = cairo_bits_append(out, out_bytes * 8, bit_pos, f.bits.data(), f.nbits);
     else
       *bit_pos += f.nbits;  // count only
+    // the caller's buffer is too small: keep the payload, so a collect with a
+    // larger buffer (cairo_stream_payload_bits tells how large) still gets it
+    if (r == kCapacityLimit) return r;
   }
   {
     std::lock_guard<std::mutex> lk(s->m);
@@ -289,6 +292,25 @@ int cairo_stream_collect(cairo_stream* s, int ticket, uint8_t* out, uint64_t out
   }
   s->cv.notify_all();
   return r;
+}
+
+int cairo_stream_payload_bits(cairo_stream* s, int ticket, uint64_t* nbits) {
+  if (!s || ticket < 0 || !nbits) return kInvalidArg;
+  Frame& f = s->at(ticket);
+  bool pending;
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    if (f.ticket != ticket || f.state == Frame::kFree) return kInvalidResource;
+    pending = f.state == Frame::kSubmitted;
+  }
+  if (pending) {
+    const int r = cairo::ctx_flush(s->ctx, ticket);
+    if (r) return r;
+  }
+  std::unique_lock<std::mutex> lk(s->m);
+  s->cv.wait(lk, [&] { return f.state == Frame::kDone; });
+  *nbits = f.nbits;
+  return f.status;
 }
 
 int cairo_stream_timeline(cairo_stream* s, int ticket, double* t) {

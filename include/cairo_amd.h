@@ -50,8 +50,15 @@ typedef struct cairo_frame_result {
  * R = EVX_REFERENCE_FRAME_COUNT (1..4); device is the HIP ordinal. */
 CAIRO_API int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
                                cairo_ctx **out);
+/* The same with an explicit number of staging slots (frames in flight,
+ * 2..256; cairo_ctx_create uses 64).  A synchronous caller (one frame in
+ * flight, as evx1_encoder::encode) needs 2: about 0.35 GB of HBM for a 4K
+ * R = 4 context instead of 8 GB.  Frames per launch are at most stages / 2. */
+CAIRO_API int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int device,
+                                  int stages, cairo_ctx **out);
 CAIRO_API int cairo_ctx_destroy(cairo_ctx *ctx);
-/* Zero every plane (fresh-encoder state, common.cpp:79-150). */
+/* Zero every plane (fresh-encoder state, common.cpp:79-150) and clear a
+ * reported in-kernel timeout, so the context is usable again. */
 CAIRO_API int cairo_ctx_reset(cairo_ctx *ctx);
 
 /* Submit frame (index, type 0=intra/1=inter, quality).  rgb is RGB888 with
@@ -99,7 +106,10 @@ CAIRO_API int cairo_ctx_read_table(cairo_ctx *ctx, uint8_t *table);
 CAIRO_API int cairo_ctx_set_debug(cairo_ctx *ctx, int flags);
 CAIRO_API int cairo_ctx_read_stamps(cairo_ctx *ctx, uint64_t *out);
 /* Debug: flags & 4 keeps a live per-workgroup state trace of the engine in
- * mapped host memory; read it (n int32 words) without synchronizing. */
+ * mapped host memory; read it (n int32 words) without synchronizing.
+ * flags & 8 (test hook) marks the device's sticky timeout word as if an
+ * in-kernel wait had timed out: every later frame reports
+ * EVX_ERROR_HARDWAREFAIL until cairo_ctx_reset. */
 CAIRO_API int cairo_ctx_read_trace(cairo_ctx *ctx, int32_t *out, int n);
 CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, int16_t *v);
 
@@ -107,9 +117,16 @@ CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, 
 CAIRO_API int cairo_ctx_set_profiling(cairo_ctx *ctx, int enable);
 /* Accumulated ms per kernel since the last call: [convert, 0 (inter search
  * runs inside the engine), engine (inter search + row coding + in-loop
- * deblock)], and the number of frames they cover; resets the accumulators. */
-CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[3], int *frames);
-/* Row-coder workgroups of the engine (0 = automatic). */
+ * deblock) summed over launches, engine busy time = the length of the union
+ * of the launches' intervals (two launches run at once, so the sum counts
+ * overlapped time twice)], and the number of frames they cover; resets the
+ * accumulators.  Enabling profiling starts the common clock of the busy
+ * intervals. */
+CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[4], int *frames);
+/* Row-coder workgroups of the engine per launch (0 = automatic: a quarter of
+ * the device's resident engine workgroups, 192 on a full MI355X; larger
+ * values are rejected, since every launch must stay co-resident with the
+ * one before it). */
 CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows);
 
 /* Known-answer check of the device transform chain: count macroblocks of 384
@@ -156,9 +173,13 @@ CAIRO_API int cairo_stream_create(cairo_ctx *ctx, int threads, cairo_stream **ou
 CAIRO_API int cairo_stream_submit(cairo_stream *s, const uint8_t *rgb, int rgb_on_device,
                                   uint32_t index, uint32_t type, uint32_t quality, int *ticket);
 /* Wait for the frame's payload and append it at bit *bit_pos of out
- * (out_bytes capacity, LSB-first; out == NULL only advances *bit_pos). */
+ * (out_bytes capacity, LSB-first; out == NULL only advances *bit_pos).  If it
+ * does not fit, returns EVX_ERROR_CAPACITY_LIMIT (7) and keeps the payload:
+ * collect again with a larger buffer. */
 CAIRO_API int cairo_stream_collect(cairo_stream *s, int ticket, uint8_t *out, uint64_t out_bytes,
                                    uint64_t *bit_pos);
+/* Wait for the frame's payload and return its size in bits (not collected). */
+CAIRO_API int cairo_stream_payload_bits(cairo_stream *s, int ticket, uint64_t *nbits);
 /* Diagnostic timeline of a collected frame (valid until ticket + 2*stages is
  * submitted): t[5] = submitted, outputs on the host, entropy start, entropy
  * end, collected; microseconds of a monotonic clock. */
@@ -178,6 +199,9 @@ CAIRO_API int evx_encoder_set_quality(void *enc, uint8_t quality);
 /* Encode one RGB888 frame, appending to the bit stream bs (evx_bitstream_*). */
 CAIRO_API int evx_encoder_encode(void *enc, const void *rgb, uint32_t width, uint32_t height,
                                  void *bs);
+/* Debug view of the last encoded frame (EVX_PEEK_STATE, evx1.h): RGB888 of
+ * the nominal frame size into rgb (evx1enc.cpp:170-305). */
+CAIRO_API int evx_encoder_peek(void *enc, int state, void *rgb);
 CAIRO_API int evx_encoder_set_ring(void *enc, uint32_t ring); /* before first encode */
 CAIRO_API int evx_encoder_set_device(void *enc, int device);  /* before first encode */
 

@@ -126,8 +126,13 @@ static void mb_copy(mbv s, mbv d) {
         }
 }
 
+/* Work counters (test infrastructure): macroblock-sized metric and lerp
+ * evaluations, for the algorithmic pixel-op count of SURVEY.md §8(d). */
+static uint64_t g_ops[4]; /* blk_sad, blk_mad, blk_sad0, mb_lerp calls */
+
 /* lerp_macroblock_half / _quarter, macroblock.h:203-241 */
 static void mb_lerp(mbv a, mbv b, mbv d, int quarter) {
+    g_ops[3]++;
     for (int j = 0; j < 16; j++)
         for (int i = 0; i < 16; i++) {
             int32_t t;
@@ -163,6 +168,7 @@ static void mb_lerp(mbv a, mbv b, mbv d, int quarter) {
 /* compute_block_sad(left, right), analysis.h:42-55 */
 static int32_t blk_sad(mbv a, mbv b) {
     int32_t s = 0;
+    g_ops[0]++;
     for (int j = 0; j < 16; j++)
         for (int i = 0; i < 16; i++) s += iabs32(a.y[j * a.stride + i] - b.y[j * b.stride + i]);
     return s;
@@ -170,6 +176,7 @@ static int32_t blk_sad(mbv a, mbv b) {
 /* compute_block_sad(delta), analysis.h:57-68 */
 static int32_t blk_sad0(mbv a) {
     int32_t s = 0;
+    g_ops[2]++;
     for (int j = 0; j < 16; j++)
         for (int i = 0; i < 16; i++) s += iabs32(a.y[j * a.stride + i]);
     return s;
@@ -177,6 +184,7 @@ static int32_t blk_sad0(mbv a) {
 /* compute_block_mad, analysis.h:103-125 (luma then chroma) */
 static int32_t blk_mad(mbv a, mbv b) {
     int32_t m = 0;
+    g_ops[1]++;
     for (int j = 0; j < 16; j++)
         for (int i = 0; i < 16; i++) {
             int32_t t = iabs32(a.y[j * a.stride + i] - b.y[j * b.stride + i]);
@@ -1249,4 +1257,13 @@ uint64_t orc_fnv1a64(uint64_t h, const uint8_t *d, uint64_t n) {
         h *= 0x100000001b3ull;
     }
     return h;
+}
+
+/* Work counters since the last reset: [blk_sad, blk_mad, blk_sad0, mb_lerp]
+ * calls (256, 384, 256 and 384 pixel operations each). */
+void orc_op_counts(uint64_t out[4], int reset) {
+    for (int k = 0; k < 4; k++) {
+        if (out) out[k] = g_ops[k];
+        if (reset) g_ops[k] = 0;
+    }
 }

@@ -77,6 +77,10 @@ void orc_deblock(const uint8_t *block_table, int16_t *y, int16_t *u, int16_t *v,
 
 /* band4 synthetic content, RGB888 tightly packed. */
 void orc_make_frame(uint8_t *rgb, int w, int h, uint32_t t, uint32_t seed);
+/* Work counters since the last reset (process-wide): calls of the SAD, MAD,
+ * zero-SAD and lerp macroblock helpers (256, 384, 256 and 384 pixel
+ * operations each), for the algorithmic op count of SURVEY.md §8(d). */
+void orc_op_counts(uint64_t out[4], int reset);
 /* FNV-1a-64 over bytes, continuing from h. */
 uint64_t orc_fnv1a64(uint64_t h, const uint8_t *data, uint64_t n);
 

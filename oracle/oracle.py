@@ -66,6 +66,7 @@ def lib() -> ctypes.CDLL:
         L.orc_dequantize_mb.argtypes = [ctypes.c_uint8, I, P, P, P, P, P, P]
         L.orc_deblock.argtypes = [P, P, P, P, I, I]
         L.orc_convert_rgb.argtypes = [P, I, I, P, P, P, I, I]
+        L.orc_op_counts.argtypes = [P, I]
         _lib = L
     return _lib
 
@@ -84,6 +85,19 @@ def make_frame(w: int, h: int, t: int, seed: int = 1234) -> np.ndarray:
 def fnv1a64(data: bytes, h: int = FNV_OFFSET) -> int:
     buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
     return lib().orc_fnv1a64(h, _ptr(np.ascontiguousarray(buf)), len(data))
+
+
+PIXEL_OPS_PER_CALL = (256, 384, 256, 384)  # SAD, MAD, zero-SAD, lerp
+
+
+def op_counts(reset: bool = False) -> dict:
+    """Oracle work since the last reset: helper calls and the algorithmic
+    pixel-op total (one abs-difference, max or lerp per pixel)."""
+    out = np.zeros(4, np.uint64)
+    lib().orc_op_counts(_ptr(out), int(reset))
+    calls = [int(x) for x in out]
+    return {"sad": calls[0], "mad": calls[1], "sad0": calls[2], "lerp": calls[3],
+            "pixel_ops": sum(c * k for c, k in zip(calls, PIXEL_OPS_PER_CALL))}
 
 
 def canonical_frame_bytes(data: bytes, nbits: int, first: bool) -> bytes:

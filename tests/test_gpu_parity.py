@@ -228,7 +228,11 @@ def test_encoder_stream_matches_golden(orc, cairo, cfg):
 # the GPU with row-level dependencies); every frame must still match.
 # ---------------------------------------------------------------------------
 
-def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None):
+def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None, workgroups=0):
+    """Frames through one pipelined Context (up to `stages` in flight, `batch`
+    frames per launch, 0 = the library default; consecutive launches overlap
+    on two streams) vs the oracle: block table and coefficients of every
+    frame, then every ring slot at the end."""
     gen = gen or orc.make_frame
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
@@ -242,8 +246,11 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
         ref.append((intra, e.block_table(), e.planes(1)))
     final_slots = [e.planes(2 + k) for k in range(ring)]
     ctx = cairo.Context(w, h, ring)
-    ctx.set_batch(batch)
-    stages = ctx.L.cairo_ctx_stages(ctx.h)
+    if batch:
+        ctx.set_batch(batch)
+    if workgroups:
+        ctx.set_workgroups(workgroups)
+    stages = ctx.stages
     pending = []
 
     def check(t, tk):

@@ -1,0 +1,231 @@
+"""GPU parity of the configurations bench.py times, and of the drop-in API.
+
+* The pipelined Context with the library's default frames per launch (32 at
+  720p, 12 at 1080p, 16 at 4K), several launches in flight on two streams and,
+  above 4000 macroblocks, helper issue priority: exactly what bench.py's
+  timed region runs (BASELINE.json configs[1..4]), frame by frame against the
+  oracle (block table, coefficients) and every ring slot at the end.
+* evx1_encoder::encode() called from C++ through the vtable
+  (tests/api/evx1_api_caller.cpp, built against include/evx1.h), peek() views,
+  periodic intra (evx1enc.cpp:143-150), recovery after a reported timeout, the
+  synchronous encoder's memory footprint, and reduced worker pools.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import _run_batched, _table_equal
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+API_BIN = os.path.join(ROOT, "cairo_amd", "_lib", "evx1_api_caller")
+
+
+# ---------------------------------------------------------------------------
+# The timed configurations, library defaults
+# ---------------------------------------------------------------------------
+
+def test_timed_720p_default_batch(orc, cairo):
+    """configs[1]: 720p q=16 R=2, default 32 frames per launch, 40 frames = a
+    full launch + a partial one overlapping it."""
+    assert cairo.default_batch(1280, 720) == 32
+    _run_batched(orc, cairo, 1280, 720, 2, 16, 40, 0)
+
+
+def test_timed_1080p_default_batch(orc, cairo):
+    """configs[2]: 1080p q=8 R=4 (8 zero rows of padding), default 12 frames
+    per launch, 16 frames: all three references live, two overlapping launches."""
+    assert cairo.default_batch(1920, 1080) == 12
+    _run_batched(orc, cairo, 1920, 1080, 4, 8, 16, 0)
+
+
+def test_timed_4k_default_batch(orc, cairo):
+    """configs[3] on one GPU: 4K q=16 R=4, default 16 frames per launch with
+    helper priority, 18 frames: two overlapping launches, 3 live references."""
+    assert cairo.default_batch(3840, 2160) == 16
+    _run_batched(orc, cairo, 3840, 2160, 4, 16, 18, 0)
+
+
+@pytest.mark.parametrize("q", [1, 8, 31])
+def test_4k_quality_sweep(orc, cairo, q):
+    """configs[4]: the 4K quality sweep (VAQ on), default launch."""
+    _run_batched(orc, cairo, 3840, 2160, 4, q, 3, 0)
+
+
+@pytest.mark.parametrize("rows", [1, 3])
+def test_reduced_worker_pools(orc, cairo, rows):
+    """One or three row coders / helpers per launch (a partly resident launch
+    degenerates to this): the task queues still drain in dependency order."""
+    _run_batched(orc, cairo, 352, 288, 4, 16, 10, 4, workgroups=rows)
+
+
+def test_workgroup_cap(cairo):
+    ctx = cairo.Context(352, 288, 2)
+    with pytest.raises(cairo.CairoError):
+        ctx.set_workgroups(100000)  # more than stays co-resident with the other launch
+    ctx.close()
+
+
+# ---------------------------------------------------------------------------
+# The drop-in API
+# ---------------------------------------------------------------------------
+
+def _api(args):
+    assert os.path.exists(API_BIN), "build with make (cairo_amd/_lib/evx1_api_caller)"
+    r = subprocess.run([API_BIN] + [str(a) for a in args], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_streams.json")))["configs"]
+
+
+@pytest.mark.parametrize("cfg", [c for c in GOLD if not c["intra_only"]], ids=lambda c: c["name"])
+def test_cpp_caller_matches_golden(cfg):
+    """A C++ program built against include/evx1.h drives evx1_encoder through
+    its vtable; its stream equals the frozen oracle stream."""
+    d = _api([cfg["width"], cfg["height"], cfg["ring"], cfg["quality"], cfg["frames"]])
+    assert d["frame_bits"] == cfg["frame_bits"]
+    assert d["fnv1a64"] == cfg["fnv1a64"]
+
+
+def test_cpp_caller_4k(orc, tmp_path):
+    """The drop-in API at BASELINE configs[3] geometry: three frames."""
+    w, h, ring, q, n = 3840, 2160, 4, 16, 3
+    rec = tmp_path / "rec.bin"
+    d = _api([w, h, ring, q, n, "--records", rec])
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    raw = rec.read_bytes()
+    p = 0
+    for t in range(n):
+        nb = int(np.frombuffer(raw[p:p + 4], np.uint32)[0])
+        got = raw[p + 4:p + 4 + (nb + 7) // 8]
+        p += 4 + (nb + 7) // 8
+        data, want_bits = e.encode(orc.make_frame(w, h, t))
+        assert nb == want_bits == d["frame_bits"][t], t
+        assert orc.canonical_frame_bytes(got, nb, t == 0) == orc.canonical_frame_bytes(data, nb, t == 0), t
+
+
+def test_periodic_intra(orc, cairo):
+    """evx1enc.cpp:143-150: after frame index 3599 ((index + 1) % 3600 == 0)
+    the next frame is intra.  3603 frames of one macroblock through the
+    drop-in encoder, every record against the oracle's."""
+    w = h = 16
+    enc = cairo.Encoder(ring=4)
+    enc.set_quality(16)
+    e = orc.OracleEncoder(4)
+    e.set_quality(16)
+    bs = cairo.BitStream(1 << 16)
+    types = []
+    for t in range(3603):
+        rgb = orc.make_frame(w, h, t)
+        bs.empty()
+        enc.encode(rgb, bs)
+        data, nb = e.encode(rgb)
+        got = bs.data()
+        assert bs.bits() == nb, t
+        assert orc.canonical_frame_bytes(got, nb, t == 0) == orc.canonical_frame_bytes(data, nb, t == 0), t
+        off = 14 if t == 0 else 0  # frame descriptor {type u32, index u32, quality u16}
+        types.append(int(np.frombuffer(got[off:off + 4], np.uint32)[0]))
+        assert int(np.frombuffer(got[off + 4:off + 8], np.uint32)[0]) == t
+    assert types[0] == 0 and types[3600] == 0
+    assert all(types[t] == 1 for t in range(1, 3603) if t != 3600)
+    enc.close()
+
+
+def _peek_views(orc, cairo, e, w, h, ring, index):
+    """The reference's peek() views (evx1enc.cpp:170-305) from the oracle's state."""
+    wmb = ((w + 15) // 16)
+    tb = e.block_table()
+    jj, ii = np.mgrid[0:h, 0:w]
+    d = tb[(ii // 16) + (jj // 16) * wmb]
+    copy = (d["block_type"] & 4) != 0
+    out = {}
+    v = np.zeros((h, w, 3), np.uint8)
+    v[..., 2] = 255 * copy
+    v[..., 1] = 255 * ((d["block_type"] & 2) != 0)
+    v[..., 0] = 255 * ((d["block_type"] & 1) != 0)
+    out[cairo.PEEK_BLOCK_TABLE] = v
+    v = np.zeros((h, w, 3), np.uint8)
+    qv = ((255 - 15 * d["q_index"].astype(np.int32)) & 255).astype(np.uint8)
+    for c in range(3):
+        v[..., c] = np.where(copy, 255 if c == 0 else 0, qv)
+    out[cairo.PEEK_QUANT_TABLE] = v
+    v = np.zeros((h, w, 3), np.uint8)
+    var = np.clip(np.trunc(d["variance"].astype(np.int32) / 30), 0, 255).astype(np.uint8)
+    for c in range(3):
+        v[..., c] = np.where(copy, 255 if c == 0 else 0, var)
+    out[cairo.PEEK_BLOCK_VARIANCE] = v
+    v = np.zeros((h, w, 3), np.uint8)
+    sp = d["sp_pred"] != 0
+    v[..., 1] = np.where(sp, 255 * d["sp_amount"], 0)
+    v[..., 2] = np.where(sp, 255 * (d["sp_amount"] == 0), 0)
+    out[cairo.PEEK_SPMP_TABLE] = v
+    out[cairo.PEEK_SOURCE] = cairo.yuv_to_rgb(*e.planes(0), w, h)
+    out[cairo.PEEK_DESTINATION] = cairo.yuv_to_rgb(*e.planes(2 + index % ring), w, h)
+    return out
+
+
+def test_peek_views(orc, cairo):
+    """peek() of every implemented state after each of 4 frames (I + 3 P),
+    ragged size; PREDICTION is not implemented in the reference either."""
+    w, h, ring, q = 200, 120, 4, 8
+    enc = cairo.Encoder(ring=ring)
+    enc.set_quality(q)
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    bs = cairo.BitStream(w * h * 64 + 65536)
+    for t in range(4):
+        rgb = orc.make_frame(w, h, t)
+        bs.empty()
+        enc.encode(rgb, bs)
+        e.encode(rgb)
+        for state, want in _peek_views(orc, cairo, e, w, h, ring, t).items():
+            np.testing.assert_array_equal(enc.peek(state, w, h), want, err_msg=f"frame {t} peek state {state}")
+        with pytest.raises(cairo.CairoError):
+            enc.peek(cairo.PEEK_PREDICTION, w, h)
+    enc.close()
+
+
+def test_reset_recovers_after_timeout(orc, cairo):
+    """A reported in-kernel timeout (the sticky word, set here by the test
+    hook) fails every frame until cairo_ctx_reset, which restores a
+    fresh-encoder state (common.cpp:79-150): the next stream is bit-exact."""
+    w, h, ring, q = 352, 288, 2, 16
+    ctx = cairo.Context(w, h, ring)
+    ctx.encode_frame(orc.make_frame(w, h, 0), 0, False, q)
+    ctx.set_debug(8)
+    with pytest.raises(cairo.CairoError) as ei:
+        ctx.encode_frame(orc.make_frame(w, h, 1), 1, True, q)
+    assert ei.value.status == cairo.EVX_ERROR_HARDWAREFAIL
+    cairo.lib().cairo_ctx_reset(ctx.h)
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    for t in range(3):
+        rgb = orc.make_frame(w, h, t)
+        e.encode(rgb)
+        out = ctx.encode_frame(rgb, t, t > 0, q)
+        _table_equal(out.table, e.block_table(), f"after reset, frame {t}")
+        np.testing.assert_array_equal(out.coef_y, e.planes(1)[0])
+    ctx.close()
+
+
+def test_sync_encoder_memory_4k(cairo):
+    """The synchronous drop-in encoder keeps 2 staging slots: a 4K R=4
+    instance takes well under 1 GB of HBM (64 slots would be about 8 GB)."""
+    import torch
+
+    torch.cuda.init()
+    free0, _ = torch.cuda.mem_get_info()
+    enc = cairo.Encoder(ring=4)
+    enc.set_quality(16)
+    bs = cairo.BitStream(3840 * 2160 * 64)
+    enc.encode(cairo.make_band4(3840, 2160, 0), bs)
+    free1, _ = torch.cuda.mem_get_info()
+    enc.close()
+    used = free0 - free1
+    assert used < 1 << 30, f"{used / 2**20:.0f} MiB"

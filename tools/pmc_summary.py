@@ -14,7 +14,10 @@ HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are KiB per dispatch; on gfx950 FETCH_SIZE counts half the bytes of
 wide streaming reads, so it is doubled; WRITE_SIZE is taken as is.  The median
 over the P-frame dispatches is reported (the first frame is intra-only).
-usage: python tools/pmc_summary.py --round r01 --config 720p [--src gpurun_out]
+The kernel trace gives the engine's busy time per frame (union of the timed
+launches' intervals / frames) and the roofline fraction it implies, the same
+computation bench.py makes from HIP events.
+usage: python tools/pmc_summary.py --round r02 --config 4k [--src gpurun_out/prof_4k]
 """
 import argparse
 import csv
@@ -71,11 +74,25 @@ def wave_states(path):
     return out
 
 
+def union_ns(iv):
+    """Length of the union of sorted [start, end) intervals."""
+    total, s0, e0 = 0, None, None
+    for s, e in iv:
+        if e0 is None or s > e0:
+            if e0 is not None:
+                total += e0 - s0
+            s0, e0 = s, e
+        else:
+            e0 = max(e0, e)
+    return total + (e0 - s0 if e0 is not None else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r01")
     ap.add_argument("--config", default="720p")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--steps", type=int, default=20, help="timed launches of the profiled bench.py run")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per engine launch in the profiled run (0: the library default for --config)")
     a = ap.parse_args()
@@ -109,12 +126,22 @@ def main():
         res["per_frame_hbm_bytes"][k] = int(round((2 * f + w) * 1024 / a.batch))
         res["dispatches"][k] = min(len(fetch[k]), len(write[k]))
     trace = os.path.join(a.src, "prof_kt", "run_kernel_trace.csv")
-    if os.path.exists(trace):  # engine time per frame, to set beside bench.py's roofline.avg_ms
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
-                if "::k_engine<false>(" in r["Kernel_Name"]]
-        if len(durs) > 2:
-            full = durs[1:-1]  # without the first (intra frame) and the last (partial) launch
-            res["engine_ms_per_frame_rocprof"] = round(statistics.median(full) / 1e6 / a.batch, 4)
+    if os.path.exists(trace):  # the same figures as bench.py's roofline, from the dispatch timestamps
+        iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace))
+                    if "::k_engine<false>(" in r["Kernel_Name"])
+        timed = iv[-a.steps:]  # bench.py's timed launches follow the warm-up ones (ctx.sync between)
+        if timed:
+            busy = union_ns(timed) / 1e6
+            res["engine_timed_launches"] = len(timed)
+            res["engine_avg_launch_ms_rocprof"] = round(statistics.mean(e - s for s, e in timed) / 1e6, 3)
+            res["engine_busy_ms_per_frame_rocprof"] = round(busy / (len(timed) * a.batch), 4)
+            sys.path.insert(0, ROOT)
+            from bench import CONFIGS, HBM_PEAK_GBS, algorithmic_bytes
+
+            w, h, ring = CONFIGS[a.config][:3]
+            ab = algorithmic_bytes(w, h, ring)["engine"]
+            res["roofline_frac_rocprof"] = round(ab / (res["engine_busy_ms_per_frame_rocprof"] * 1e-3) / 1e9 /
+                                                 HBM_PEAK_GBS, 6)
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws
