@@ -142,6 +142,15 @@ def main():
             ab = algorithmic_bytes(w, h, ring)["engine"]
             res["roofline_frac_rocprof"] = round(ab / (res["engine_busy_ms_per_frame_rocprof"] * 1e-3) / 1e9 /
                                                  HBM_PEAK_GBS, 6)
+    log = os.path.join(a.src, "prof_kt.log")
+    if os.path.exists(log):  # bench.py's own HIP-event figures in the traced run (must agree with the trace)
+        lines = [ln for ln in open(log) if ln.startswith('{"metric"')]
+        if lines:
+            b = json.loads(lines[-1])
+            res["bench_under_trace"] = {"value": b["value"], "ms_per_step": b["ms_per_step"],
+                                        "engine_busy_ms_per_frame": b["roofline"]["engine_busy_ms_per_frame"],
+                                        "avg_launch_ms": b["roofline"]["avg_launch_ms"],
+                                        "frac": b["roofline"]["frac"]}
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws
