@@ -96,9 +96,7 @@ struct cairo_ctx {
   hipStream_t ks2 = nullptr;         // launches alternate between ks and ks2 (consecutive batches overlap)
   hipEvent_t engine_done = nullptr;  // last launched batch finished (copy stream waits on it)
   hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k
-  hipEvent_t area_ready[kSyncAreas] = {}; // the launch using area k has zeroed it
   long long batches = 0;             // launches so far
-  int prev_nframes = 0;              // frames of the previous launch
   // per-slot device buffers
   int16_t *src = nullptr, *coef = nullptr;
   BlockDesc *table = nullptr, *idesc = nullptr;
@@ -106,6 +104,8 @@ struct cairo_ctx {
   uint64_t* gran = nullptr;
   uint8_t* rgb = nullptr;
   int16_t* ring_buf = nullptr;
+  uint64_t* progress = nullptr;  // [stages][hmb] tagged deblock progress of each slot's frame
+  bool fresh = true;             // no frame since create / reset: the next has no predecessor
   int32_t *sync = nullptr, *sticky = nullptr;
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
   FrameArgs* fdesc_host = nullptr;  // pinned [kLaunchSlots][kMaxBatch]: per-frame views per launch
@@ -179,7 +179,6 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.idesc_base = c->idesc;
   e.isad_base = c->isad;
   e.gran_base = c->gran;
-  e.ring_base = c->ring_buf;
   e.sync = c->sync;
   e.sticky = c->sticky;
   e.stamps = c->stamps;
@@ -207,11 +206,9 @@ void free_ctx(cairo_ctx* c) {
   if (c->t_base) (void)hipEventDestroy(c->t_base);
   for (auto& ev : c->batch_end)
     if (ev) (void)hipEventDestroy(ev);
-  for (auto& ev : c->area_ready)
-    if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
-  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad,
+  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps})
     (void)hipFree(p);
@@ -233,12 +230,13 @@ int zero_state(cairo_ctx* c) {
   // granule tags start at 0; the n-th submission after a reset publishes tag n
   CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * S, c->ks));
   CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t) * kSyncAreas, c->ks));
+  CK(hipMemsetAsync(c->progress, 0, (size_t)c->hmb * sizeof(uint64_t) * S, c->ks));
   CK(hipMemsetAsync(c->sticky, 0, sizeof(int32_t), c->ks));
   CK(hipStreamSynchronize(c->ks));
   c->epoch = 0;
   c->last_slot = -1;
-  c->batches = 0;  // the first launch after a reset depends on no earlier launch
-  c->prev_nframes = 0;
+  c->batches = 0;
+  c->fresh = true;  // the first frame after a reset depends on no earlier frame
   for (auto& s : c->st) *s.err = 0;
   return kSuccess;
 }
@@ -278,11 +276,11 @@ int flush(cairo_ctx* c) {
   e.fa = fd;
   e.decode = c->pend[0].decode;  // a launch never mixes (decode_frame flushes first)
   const int rows = e.nframes * e.hmb;
-  const int ng = (e.wmb + 3) / 4;
   (void)any_inter;
   // Launch b alternates streams and sync areas; it follows launch b-1, which
-  // may still be running: its frame 0 reads the deblock progress of b-1's last
-  // frame.  Residency: a launch takes at most half of the engine's resident
+  // may still be running: its frame 0 waits on the deblock progress of b-1's
+  // last frame (tagged words in that frame's staging slot).  Residency: a
+  // launch takes at most half of the engine's resident
   // workgroup slots (CUs x occupancy, measured at create: 256 x 3 = 768 on a
   // full MI355X), so two launches are always co-resident.  Every row has a
   // coder and a helper (inter search + deblock) living as long as the row:
@@ -291,21 +289,13 @@ int flush(cairo_ctx* c) {
   hipStream_t st = (b & 1) ? c->ks2 : c->ks;
   const int area = (int)(b % kSyncAreas);
   e.sync = c->sync + (size_t)area * c->sync_words;
-  e.prev_last_deblocked =
-      b > 0 ? c->sync + (size_t)((b - 1) % kSyncAreas) * c->sync_words +
-                  SyncLayout::deblocked((int)c->hmb, ng, c->prev_nframes - 1)
-            : nullptr;
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
-  c->prev_nframes = e.nframes;
   e.n_rows = c->wg_rows > 0 ? std::min(c->wg_rows, c->max_rows) : c->max_rows;
   if (e.n_rows > rows) e.n_rows = rows;
   e.n_helpers = e.n_rows;
-  // this sync area was last used by launch b-3 and read by launch b-2
-  if (b >= 2) CK(hipStreamWaitEvent(st, c->batch_end[(b - 2) % kSyncAreas], 0));
+  // this sync area was last used by launch b-3 (only a launch reads its own
+  // area); launch b-2 precedes this one on the same stream
   if (b >= 3) CK(hipStreamWaitEvent(st, c->batch_end[(b - 3) % kSyncAreas], 0));
-  // ...and this launch reads launch b-1's area: b-1 must have zeroed it first
-  // (otherwise the words still say "done" from launch b-4)
-  if (b >= 1) CK(hipStreamWaitEvent(st, c->area_ready[(b - 1) % kSyncAreas], 0));
   TimedBatch* tb = nullptr;
   if (c->profiling) {
     tb = &c->tb[c->tb_next];
@@ -326,7 +316,6 @@ int flush(cairo_ctx* c) {
   }
   CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(e.sync, 0, c->sync_words * sizeof(int32_t), st));
-  CK(hipEventRecord(c->area_ready[area], st));
   if (c->stamps) {  // engine entry (min) / exit (max) words
     static const uint64_t init[2] = {~0ull, 0};
     CK(hipMemcpyAsync(c->stamps + kMaxBatch * stamp_frame_words((int)c->wmb, (int)c->hmb), init, sizeof(init),
@@ -366,6 +355,21 @@ int flush(cairo_ctx* c) {
   c->npend = 0;
   c->launched_cv.notify_all();
   return kSuccess;
+}
+
+// The cross-frame views of the frame submitted as ticket t (FrameDesc):
+// ring slots by index (common.cpp:192-195), the previous ticket's staging
+// slot for the output_cache chain and its deblock progress.
+void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
+  const int R = (int)c->ring;
+  for (int k = 0; k < kMaxRing; k++)
+    f.recon[k] = slot_planes(c->ring_buf, c, k < R ? (int)(((uint32_t)f.index + R - k) % R) : 0);
+  f.stale = f.recon[0];
+  const int ps = (t + c->stages - 1) % c->stages;
+  f.coef_prev = slot_planes(c->coef, c, ps);
+  f.progress = c->progress + (size_t)f.slot * c->hmb;
+  f.prev_progress = c->fresh ? nullptr : c->progress + (size_t)ps * c->hmb;
+  c->fresh = false;
 }
 
 int sync_all(cairo_ctx* c) {
@@ -445,6 +449,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipMalloc(&c->gran, c->mbs * kGranuleStride * sizeof(uint64_t) * S));
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * S));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t) * kSyncAreas));
+  TRY(hipMalloc(&c->progress, (size_t)c->hmb * sizeof(uint64_t) * S));
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
   {  // (frame, row) task order of the engine pools, for every batch size
@@ -475,7 +480,6 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipEventCreateWithFlags(&c->engine_done, hipEventDisableTiming));
   TRY(hipEventCreate(&c->t_base));
   for (auto& ev : c->batch_end) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  for (auto& ev : c->area_ready) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 #undef TRY
   r = zero_state(c);
   if (r != kSuccess) {
@@ -586,10 +590,10 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   f.quality = (int)quality;
   f.epoch = ++c->epoch;
   f.slot = slot;
-  f.prev_slot = (t + c->stages - 1) % c->stages;
   f.decode = 0;  // decode_frame never leaves a decode frame pending
   f.host_table = nullptr;
   f.host_coef = nullptr;
+  frame_links(c, f, t);
   c->npend++;
   s.busy = true;
   s.launched = false;
@@ -673,8 +677,8 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
   f.quality = 1;
   f.epoch = ++c->epoch;
   f.slot = slot;
-  f.prev_slot = (t + c->stages - 1) % c->stages;
   f.decode = 1;
+  frame_links(c, f, t);
   f.host_table = reinterpret_cast<const BlockDesc*>(table);
   f.host_coef = coef;
   c->npend = 1;

@@ -60,8 +60,15 @@ struct FrameDesc {
   int quality;         // 1..31
   uint32_t epoch;      // granule tag (per-context submission count, never 0)
   int slot;            // staging slot: this frame's source / coefficient / table / granule buffers
-  int prev_slot;       // staging slot of the previous frame (output_cache chain)
   int decode;          // 1: reconstruct from the slot's table + coefficients (the decoder), no search
+  // Cross-frame state, resolved by the host (one context: its ring and
+  // staging slots; a frame-interleaved group: the owners' buffers, kernels.h
+  // FrameArgs):
+  PlaneSet recon[kMaxRing];  // [0] this frame's reconstruction, [off] the reference at offset off
+  PlaneSet stale;            // frame index-R's deblocked output (the rows below the intra search)
+  PlaneSet coef_prev;        // the previous frame's output_cache (copy-macroblock chain)
+  uint64_t* progress;        // this frame's deblock progress words [hmb]
+  const uint64_t* prev_progress;  // the previous frame's (nullptr: none, first frame after a reset)
   const BlockDesc* host_table;  // decode: the frame's block table and coefficient planes (y, u, v
   const int16_t* host_coef;     //   contiguous), uploaded at launch
 };
@@ -80,8 +87,15 @@ struct FrameArgs {
   PlaneSet in;         // input_cache of this frame
   PlaneSet coef;       // output_cache of this frame (persistent semantics: copy MBs carry coef_prev)
   PlaneSet coef_prev;  // output_cache of the previous frame
-  int16_t* ring_base;  // R contiguous reconstruction slots
-  size_t slot_elems;
+  // Reconstruction buffers: [0] this frame's (written only by its deblock),
+  // [off] = frame index-off for off = 1..R-1 (inter references; zero images
+  // before the stream start).  In one context these are ring slots
+  // (index-off) % R (common.cpp:192-195).
+  PlaneSet recon[kMaxRing];
+  // The rows below an intra search: frame index-R's deblocked output (zeros
+  // for the first R frames).  The reference reuses that slot in place, so this
+  // equals recon[0] whenever the group's slot arithmetic does too.
+  PlaneSet stale;
   BlockDesc* table;    // [wmb*hmb]
   BlockDesc* inter_desc;  // [(off-1)*mbs + mb]
   int32_t* inter_sad;     // [(off-1)*mbs + mb]
@@ -91,8 +105,13 @@ struct FrameArgs {
   int ng;              // inter-search groups (4 MBs) per row
   int nref;            // inter-search tasks per group (references; 1 carrier task for intra frames)
   int32_t* inter_done; // [hmb][ng] inter-search tasks finished
-  int32_t* deblocked;  // [hmb] final luma columns per MB row (monotone)
-  const int32_t* prev_deblocked;  // the previous frame's, if it is in this batch (else nullptr)
+  // Deblock progress per MB row, tagged: (epoch << 32) | final luma columns.
+  // Frame epochs of a stream are consecutive, so the previous frame's words
+  // are compared against (epoch - 1) << 32 | need; a staging slot's words are
+  // never cleared between frames (a later frame's larger tag also means the
+  // earlier frame is final there), so no launch ordering guards them.
+  uint64_t* progress;             // [hmb] this frame's
+  const uint64_t* prev_progress;  // [hmb] the previous frame's (nullptr: none)
   uint64_t* stamps;    // diagnostic (nullptr = off)
   uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, kIStamps stamps (see kernels.hip)
   const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)
@@ -102,20 +121,16 @@ struct FrameArgs {
 struct EngineArgs;
 FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j);
 
-// Words of the batch sync area (int32, zeroed per batch).  ng = inter-search
-// groups per MB row ((wmb + 3) / 4).
+// Words of the batch sync area (int32, zeroed per batch, read only by the
+// launch itself).  ng = inter-search groups per MB row ((wmb + 3) / 4).
 struct SyncLayout {
   static constexpr int kErr = 0;
   static constexpr int kTicketRows = 2;
   static constexpr int kTicketHelpers = 3;
   static constexpr int kFlags = 8;
-  // per frame j: inter_done[hmb][ng] (tasks finished per group), then
-  // deblocked[hmb] (luma columns of the MB row that are final)
-  __host__ __device__ static int frame_words(int hmb, int ng) { return hmb * (ng + 1); }
+  // per frame j: inter_done[hmb][ng] (tasks finished per group)
+  __host__ __device__ static int frame_words(int hmb, int ng) { return hmb * ng; }
   __host__ __device__ static int inter_done(int hmb, int ng, int j) { return kFlags + frame_words(hmb, ng) * j; }
-  __host__ __device__ static int deblocked(int hmb, int ng, int j) {
-    return kFlags + frame_words(hmb, ng) * j + hmb * ng;
-  }
   __host__ __device__ static int words(int hmb, int ng) { return kFlags + frame_words(hmb, ng) * kMaxBatch + 8; }
 };
 
@@ -132,10 +147,7 @@ struct EngineArgs {
   BlockDesc* idesc_base;   // stride nref * mbs
   int32_t* isad_base;      // stride nref * mbs
   uint64_t* gran_base;     // stride mbs * kGranuleStride
-  int16_t* ring_base;      // R reconstruction slots, stride plane_elems
   int32_t* sync;           // SyncLayout words of this launch
-  const int32_t* prev_last_deblocked;  // deblock progress words of the frame before frame 0,
-                                       // if it belongs to a launch that may still run (else nullptr)
   int32_t* sticky;
   uint64_t* stamps;
   int n_helpers, n_rows;   // worker pools (workgroups, equal sizes), interleaved in blockIdx runs of 8

@@ -27,6 +27,11 @@ namespace cairo {
 // field is fetched once (scalar loads) instead of again after every global
 // store, each refetch waiting behind the outstanding hand-off loads.
 typedef const __attribute__((address_space(4))) FrameArgs FA;
+// Reconstruction buffer k (FrameArgs::recon) of a view, selected with scalar
+// branches: a dynamically indexed struct load would go through scratch.
+#define RECON_AT(a, k)                                                                   \
+  ((k) == 1 ? planes((a).recon[1]) : (k) == 2 ? planes((a).recon[2]) : (k) == 3 ? planes((a).recon[3]) \
+                                                                              : planes((a).recon[0]))
 // A plane set field of a view, as an ordinary value.
 __host__ __device__ inline PlaneSet planes(const __attribute__((address_space(4))) PlaneSet& p) {
   PlaneSet r;
@@ -143,6 +148,15 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 __device__ __forceinline__ void stamp(FA& a, int mb, int k) {
   if (a.stamps && threadIdx.x == 0)
     a.stamps[(size_t)mb * kStampPhases + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Deblock progress words (kernels.h FrameArgs::progress): tag a column count
+// with the frame's epoch; relaxed agent-scope 64-bit loads.
+__device__ __forceinline__ uint64_t tagged(uint32_t epoch, int cols) {
+  return ((uint64_t)epoch << 32) | (uint32_t)cols;
+}
+__device__ __forceinline__ uint64_t progress_at(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
@@ -652,8 +666,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int r, int rr, int need, DbLd
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
-      if (!a.prev_deblocked ||
-          __hip_atomic_load(a.prev_deblocked + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) {
+      if (!a.prev_progress || progress_at(a.prev_progress + rr) >= tagged(a.epoch - 1, need)) {
         d = 1;
       } else if (kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
         d = 2;
@@ -701,7 +714,7 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   const int px = x * kMB, py = r * kMB, mb = r * a.wmb + x;
   const int mbs = a.wmb * a.hmb;
   const int thr = (a.quality >> 2) + 1;
-  const PlaneSet ref = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, (a.index + a.ring - off) % a.ring);
+  const PlaneSet ref = RECON_AT(a, off);
   Sel s;
   Px6 src;
   s.bx = px;
@@ -1047,8 +1060,7 @@ __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st) {
 
 __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st) {
   const int c1 = min((st.k + 1) * kDbChunk, a.wa);
-  if (r > 0 && __hip_atomic_load(&a.deblocked[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1)
-    return false;
+  if (r > 0 && progress_at(&a.progress[r - 1]) < tagged(a.epoch, c1)) return false;
   const uint64_t g = gran_ld(gran_mb(a, st.k, r) + kGranulesPerMB);  // info granule, stored last
   return (uint32_t)(g >> 32) == a.epoch;
 }
@@ -1056,11 +1068,12 @@ __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState&
 // Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs).
 __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st) {
   const int tid = threadIdx.x;
-  const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
+  const PlaneSet cs = planes(a.recon[0]);
   const int cw = a.wa >> 1;
   const int y0 = 16 * r - 4, c0y = 8 * r - 4;  // tile origins (pixel rows)
   const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
-  int32_t* prog = a.deblocked;
+  uint64_t* prog = a.progress;
+  const uint64_t above = tagged(a.epoch, 0);
   int& w0 = st.w0;
   int& hb0 = st.hb0;
   int& vb0 = st.vb0;
@@ -1070,9 +1083,9 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     const bool last = k == nch - 1;
     // ---- inputs of chunk k ----
     if (r > 0 && tid == 0) {  // rows above final through column c1
-      if (__hip_atomic_load(&prog[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1) {
+      if (progress_at(&prog[r - 1]) < (above | (uint32_t)c1)) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(&prog[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c1) {
+        while (progress_at(&prog[r - 1]) < (above | (uint32_t)c1)) {
           if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
           __builtin_amdgcn_s_sleep(1);
           if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
@@ -1188,7 +1201,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(&prog[r], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(&prog[r], above | (uint32_t)w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.stamps && tid == 0 && k < kDbStamps)
         a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps + k] = __builtin_amdgcn_s_memrealtime();
       w0 = w1;
@@ -1461,7 +1474,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
-  const PlaneSet cs = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha, a.index % a.ring);
+  const PlaneSet cs = planes(a.stale);  // the stale rows below (frame index-R)
   int32_t* err = a.err;
   const uint32_t tag = a.epoch;
   const int cw = a.wa >> 1;
@@ -1545,8 +1558,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
         inter_d[o] = uni_desc_words(idw[o]);
         inter_sad[o] = uni(isw[o]);
         const BlockDesc& d = inter_d[o];
-        const PlaneSet rp = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
-                                      (a.index + a.ring - d.prediction_target) % a.ring);
+        const PlaneSet rp = RECON_AT(a, d.prediction_target);
         const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
         int dx = 0, dy = 0;
         if (sp) frac_dir(d.sp_index, &dx, &dy);
@@ -1644,8 +1656,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
         d.q_index = (uint8_t)(uni((int)tw.w) >> 8);  // uni_desc leaves it to the quantizer
         if (!(d.block_type & kIntra)) {
           from_inter = true;
-          const PlaneSet rp = ring_slot(a.ring_base, a.slot_elems, a.wa, a.ha,
-                                        (int)(((uint32_t)a.index + a.ring - d.prediction_target) % a.ring));
+          const PlaneSet rp = RECON_AT(a, d.prediction_target);
           const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
           int dx = 0, dy = 0;
           if (sp) frac_dir(d.sp_index, &dx, &dy);
@@ -1948,9 +1959,9 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.epoch = f.epoch;
   a.in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
   a.coef = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.slot);
-  a.coef_prev = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.prev_slot);
-  a.ring_base = e.ring_base;
-  a.slot_elems = e.plane_elems;
+  a.coef_prev = f.coef_prev;
+  for (int k = 0; k < kMaxRing; k++) a.recon[k] = f.recon[k];
+  a.stale = f.stale;
   const size_t mbs = (size_t)e.wmb * e.hmb, nref = e.ring > 1 ? e.ring - 1 : 1;
   a.table = e.table_base + (size_t)f.slot * mbs;
   a.inter_desc = e.idesc_base + (size_t)f.slot * nref * mbs;
@@ -1961,8 +1972,8 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.ng = (e.wmb + 3) >> 2;
   a.nref = a.inter ? e.ring - 1 : 1;
   a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, a.ng, j);
-  a.deblocked = e.sync + SyncLayout::deblocked(e.hmb, a.ng, j);
-  a.prev_deblocked = j > 0 ? e.sync + SyncLayout::deblocked(e.hmb, a.ng, j - 1) : e.prev_last_deblocked;
+  a.progress = f.progress;
+  a.prev_progress = f.prev_progress;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   {
     const int ng = (e.wmb + 3) / 4;
