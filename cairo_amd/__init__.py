@@ -36,6 +36,7 @@ BLOCK_DESC = np.dtype(
 assert BLOCK_DESC.itemsize == 16
 
 EVX_SUCCESS = 0
+PEER_SIZE = 3 * 4 + 5 * 4 + 3 * 8 + 3 * 64  # sizeof(cairo_peer)
 # EVX_PEEK_STATE (reference evx1.h:55-64)
 PEEK_SOURCE, PEEK_PREDICTION, PEEK_BLOCK_TABLE, PEEK_QUANT_TABLE, PEEK_SPMP_TABLE, PEEK_BLOCK_VARIANCE, \
     PEEK_DESTINATION = range(7)
@@ -83,6 +84,10 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
         "cairo_ctx_set_workgroups": (I, [P, I]),
         "cairo_ctx_set_batch": (I, [P, I]),
+        "cairo_ctx_peer_info": (I, [P, I, P]),
+        "cairo_ctx_join_group": (I, [P, I, I, P]),
+        "cairo_ctx_flush": (I, [P]),
+        "cairo_ctx_max_workgroups": (I, [P]),
         "cairo_default_batch": (I, [U, U]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
@@ -317,6 +322,83 @@ class Context:
 
     def set_workgroups(self, rows: int = 0) -> None:
         _ck(self.L.cairo_ctx_set_workgroups(self.h, rows), "set_workgroups")
+
+    def max_workgroups(self) -> int:
+        return int(self.L.cairo_ctx_max_workgroups(self.h))
+
+    def flush(self) -> None:
+        _ck(self.L.cairo_ctx_flush(self.h), "cairo_ctx_flush")
+
+    # ---- frame-interleaved groups (include/cairo_amd.h) ----
+    def peer_info(self, cross_device: bool = False) -> bytes:
+        """This member's cairo_peer record (plain bytes, to exchange)."""
+        rec = (ctypes.c_uint8 * PEER_SIZE)()
+        _ck(self.L.cairo_ctx_peer_info(self.h, int(cross_device), rec), "cairo_ctx_peer_info")
+        return bytes(rec)
+
+    def join_group(self, rank: int, peers: list) -> None:
+        """Join the group of len(peers) members as `rank` (records in rank order)."""
+        buf = b"".join(peers)
+        assert len(buf) == PEER_SIZE * len(peers)
+        arr = (ctypes.c_uint8 * len(buf)).from_buffer_copy(buf)
+        _ck(self.L.cairo_ctx_join_group(self.h, len(peers), rank, arr), "cairo_ctx_join_group")
+
+
+def group_layout(n: int, size: int, ring: int, stages: int) -> dict:
+    """Where frame n of a frame-interleaved group of `size` members lives
+    (backend.hip frame_links): its member, that member's ticket, staging
+    slot and reconstruction slot, and whether it reconstructs in place over
+    frame n - ring (the reference's ring reuse, common.cpp:192-195)."""
+    slots = -(-ring // size)  # ceil(R / N) reconstruction slots per member
+    t = n // size
+    return {"member": n % size, "ticket": t, "staging_slot": t % stages, "recon_slot": t % slots,
+            "recon_slots": slots, "in_place": size * slots == ring}
+
+
+class Group:
+    """A frame-interleaved group of member contexts in this process (one per
+    device, or several on one device) encoding ONE stream: frame n goes to
+    member n % N (include/cairo_amd.h).  Processes that each own
+    one member exchange Context.peer_info() records themselves."""
+
+    def __init__(self, width: int, height: int, ring: int, devices, stages: int = 64, batch: int = 0):
+        self.members = [Context(width, height, ring, device=d, stages=stages) for d in devices]
+        n = len(self.members)
+        per_dev = {d: list(devices).count(d) for d in devices}
+        cross = len(per_dev) > 1
+        for m, d in zip(self.members, devices):
+            if batch:
+                m.set_batch(batch)
+            if per_dev[d] > 1:  # members on one device share its workgroup slots
+                m.set_workgroups(max(1, m.max_workgroups() // per_dev[d]))
+        recs = [m.peer_info(cross_device=cross) for m in self.members]
+        for r, m in enumerate(self.members):
+            m.join_group(r, recs)
+        self.size, self.ring, self.stages = n, ring, stages
+        self.tickets = {}
+
+    def submit(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> None:
+        m = self.members[index % self.size]
+        self.tickets[index] = m.submit(rgb, index, inter, quality, on_device)
+
+    def wait(self, index: int, copy: bool = True) -> FrameOutputs:
+        """Outputs of frame `index`; launches every member's pending frames first
+        (the frame may depend on any earlier frame of the stream)."""
+        for m in self.members:
+            m.flush()
+        return self.members[index % self.size].wait(self.tickets[index], copy)
+
+    def release(self, index: int) -> None:
+        self.members[index % self.size].release(self.tickets.pop(index))
+
+    def recon(self, n: int):
+        """Frame n's deblocked reconstruction (y, u, v), while still held."""
+        lay = group_layout(n, self.size, self.ring, self.stages)
+        return self.members[lay["member"]].read_planes(2 + lay["recon_slot"])
+
+    def close(self) -> None:
+        for m in self.members:
+            m.close()
 
 
 def default_batch(width: int, height: int) -> int:

@@ -25,6 +25,7 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/cairo_amd.h"
@@ -106,6 +107,21 @@ struct cairo_ctx {
   int16_t* ring_buf = nullptr;
   uint64_t* progress = nullptr;  // [stages][hmb] tagged deblock progress of each slot's frame
   bool fresh = true;             // no frame since create / reset: the next has no predecessor
+  // Frame-interleaved group (cairo_ctx_join_group): member grank of gsize
+  // encodes the stream's frames n = grank (mod gsize), reading the others'
+  // reconstructions, output_cache and progress words in place.
+  struct Peer {
+    int16_t* ring = nullptr;
+    int16_t* coef = nullptr;
+    uint64_t* progress = nullptr;
+    int stages = 0;
+    bool imported = false;  // opened from another process's IPC handles
+  };
+  int gsize = 1, grank = 0, gbase = 0;  // gbase: ticket of the group's frame grank
+  Peer gp[kMaxGroup];
+  int16_t* zero = nullptr;  // a zero plane set: references before the stream start
+  bool fine_grained = false;  // ring / coef / progress allocated fine-grained (cross-device sharing)
+  bool sys = false;           // a member is another process or device: system-scope hand-offs
   int32_t *sync = nullptr, *sticky = nullptr;
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
   FrameArgs* fdesc_host = nullptr;  // pinned [kLaunchSlots][kMaxBatch]: per-frame views per launch
@@ -187,6 +203,41 @@ EngineArgs engine_args(const cairo_ctx* c) {
   return e;
 }
 
+// Close the group's imported peer mappings and forget the group.
+void leave_group(cairo_ctx* c) {
+  for (int i = 0; i < c->gsize; i++) {
+    cairo_ctx::Peer& p = c->gp[i];
+    if (p.imported) {
+      for (void* q : {(void*)p.ring, (void*)p.coef, (void*)p.progress})
+        if (q) (void)hipIpcCloseMemHandle(q);
+    }
+    p = cairo_ctx::Peer();
+  }
+  if (c->zero) (void)hipFree(c->zero);
+  c->zero = nullptr;
+  c->gsize = 1;
+  c->grank = 0;
+  c->sys = false;
+}
+
+// (frame, row) task order of the engine pools for every batch size, by
+// row + slope * frame (kOrderSlope for one context; a group of N members
+// needs 3N + 2: kernels.h kOrderSlope).
+std::vector<int32_t> task_order(int hmb, int slope) {
+  const int per = kMaxBatch * hmb;
+  std::vector<int32_t> ord((size_t)kMaxBatch * per, 0);
+  for (int nf = 1; nf <= kMaxBatch; nf++) {
+    int32_t* o = &ord[(size_t)(nf - 1) * per];
+    int n = 0;
+    for (int d = 0; d < hmb + slope * nf; d++)
+      for (int f = 0; f < nf; f++) {
+        const int r = d - slope * f;
+        if (r >= 0 && r < hmb) o[n++] = (f << 16) | r;
+      }
+  }
+  return ord;
+}
+
 void free_ctx(cairo_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
@@ -208,6 +259,7 @@ void free_ctx(cairo_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
+  leave_group(c);
   for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps})
@@ -362,6 +414,36 @@ int flush(cairo_ctx* c) {
 // slot for the output_cache chain and its deblock progress.
 void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
   const int R = (int)c->ring;
+  f.sys = c->sys;
+  if (c->gsize > 1) {
+    // Group member: frame m lives with member m % N as its ticket m / N
+    // (staging slot (m / N) % stages, reconstruction slot (m / N) % S with
+    // S = ceil(R / N) slots per member, so that a slot is reused only by a
+    // frame at least R later; when N * S == R that is frame m + R itself,
+    // in place, as in the reference's ring).
+    const int N = c->gsize, S = (R + N - 1) / N;
+    const long n = f.index;
+    const PlaneSet zero = planes_at(c->zero, c);
+    auto recon_of = [&](long m) {
+      if (m < 0) return zero;
+      const cairo_ctx::Peer& p = c->gp[m % N];
+      return slot_planes(p.ring, c, (int)((m / N) % S));
+    };
+    for (int k = 0; k < kMaxRing; k++) f.recon[k] = k < R ? recon_of(n - k) : zero;
+    f.stale = recon_of(n - R);
+    f.progress = c->progress + (size_t)f.slot * c->hmb;
+    if (n >= 1) {
+      const cairo_ctx::Peer& p = c->gp[(n - 1) % N];
+      const int ps = (int)(((n - 1) / N) % p.stages);
+      f.coef_prev = slot_planes(p.coef, c, ps);
+      f.prev_progress = p.progress + (size_t)ps * c->hmb;
+    } else {
+      f.coef_prev = zero;
+      f.prev_progress = nullptr;
+    }
+    c->fresh = false;
+    return;
+  }
   for (int k = 0; k < kMaxRing; k++)
     f.recon[k] = slot_planes(c->ring_buf, c, k < R ? (int)(((uint32_t)f.index + R - k) % R) : 0);
   f.stale = f.recon[0];
@@ -453,17 +535,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
   {  // (frame, row) task order of the engine pools, for every batch size
-    const int hmb = (int)c->hmb, per = kMaxBatch * hmb;
-    std::vector<int32_t> ord((size_t)kMaxBatch * per, 0);
-    for (int nf = 1; nf <= kMaxBatch; nf++) {
-      int32_t* o = &ord[(size_t)(nf - 1) * per];
-      int n = 0;
-      for (int d = 0; d < hmb + kOrderSlope * nf; d++)
-        for (int f = 0; f < nf; f++) {
-          const int r = d - kOrderSlope * f;
-          if (r >= 0 && r < hmb) o[n++] = (f << 16) | r;
-        }
-    }
+    const std::vector<int32_t> ord = task_order((int)c->hmb, kOrderSlope);
     TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch, hipHostMallocDefault));
     TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch));
     TRY(hipMalloc(&c->order, ord.size() * sizeof(int32_t)));
@@ -503,6 +575,11 @@ int cairo_ctx_reset(cairo_ctx* c) {
   int r = sync_all(c);
   if (r) return r;
   for (auto& s : c->st) s.busy = false;
+  if (c->gsize > 1) {  // a reset leaves the group (its members reset and rejoin together)
+    leave_group(c);
+    const std::vector<int32_t> ord = task_order((int)c->hmb, kOrderSlope);
+    CK(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   return zero_state(c);
 }
 
@@ -585,10 +662,16 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
     f.rgb = c->rgb + (size_t)slot * c->w * c->h * 3;
     f.host_rgb = rgb;
   }
+  if (c->gsize > 1 && (long)index != (long)(t - c->gbase) * c->gsize + c->grank) {
+    fprintf(stderr, "[cairo_amd] group member %d of %d: frame %u out of turn\n", c->grank, c->gsize, index);
+    return kInvalidArg;
+  }
   f.index = (int)index;
   f.inter = type == 1 ? 1 : 0;
   f.quality = (int)quality;
-  f.epoch = ++c->epoch;
+  // granule tag; frames of a stream have consecutive epochs (a group numbers
+  // them by stream index)
+  f.epoch = c->gsize > 1 ? index + 1 : ++c->epoch;
   f.slot = slot;
   f.decode = 0;  // decode_frame never leaves a decode frame pending
   f.host_table = nullptr;
@@ -661,6 +744,7 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
                            uint8_t* rgb) {
   if (!c || !table || !coef || !rgb) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
+  if (c->gsize > 1) return kInvalidResource;
   CK(hipSetDevice(c->device));
   int r = flush(c);  // encode frames still pending go first, in their own launch
   if (r) return r;
@@ -708,6 +792,124 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
   }
   s.busy = false;
   return r;
+}
+
+int cairo_ctx_max_workgroups(const cairo_ctx* c) { return c ? c->max_rows : 0; }
+
+int cairo_ctx_flush(cairo_ctx* c) {
+  if (!c) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  CK(hipSetDevice(c->device));
+  return flush(c);
+}
+
+int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
+  if (!c || !out) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->fresh || c->npend || c->gsize > 1) return kInvalidResource;  // before any frame, outside a group
+  CK(hipSetDevice(c->device));
+  if (cross_device && !c->fine_grained) {
+    // Memory another device reads while this one writes it: fine-grained, so
+    // that system-scope releases and acquires order it across devices.
+    const size_t S = (size_t)c->stages;
+    int16_t *ring = nullptr, *coef = nullptr;
+    uint64_t* prog = nullptr;
+    CK(hipExtMallocWithFlags((void**)&ring, c->plane_elems * 2 * c->ring, hipDeviceMallocFinegrained));
+    CK(hipExtMallocWithFlags((void**)&coef, c->plane_elems * 2 * S, hipDeviceMallocFinegrained));
+    CK(hipExtMallocWithFlags((void**)&prog, (size_t)c->hmb * sizeof(uint64_t) * S, hipDeviceMallocFinegrained));
+    CK(hipDeviceSynchronize());
+    (void)hipFree(c->ring_buf);
+    (void)hipFree(c->coef);
+    (void)hipFree(c->progress);
+    c->ring_buf = ring, c->coef = coef, c->progress = prog;
+    c->fine_grained = true;
+    int r = zero_state(c);
+    if (r) return r;
+  }
+  memset(out, 0, sizeof(*out));
+  out->width = c->w, out->height = c->h, out->ring = c->ring;
+  out->device = c->device;
+  out->pid = (int32_t)getpid();
+  out->stages = c->stages;
+  out->fine_grained = c->fine_grained;
+  out->ring_addr = (uint64_t)(uintptr_t)c->ring_buf;
+  out->coef_addr = (uint64_t)(uintptr_t)c->coef;
+  out->progress_addr = (uint64_t)(uintptr_t)c->progress;
+  void* bufs[3] = {c->ring_buf, c->coef, c->progress};
+  for (int k = 0; k < 3; k++) {
+    hipIpcMemHandle_t h;
+    CK(hipIpcGetMemHandle(&h, bufs[k]));
+    static_assert(sizeof(h) == sizeof(out->ipc[0]), "IPC handle size");
+    memcpy(out->ipc[k], &h, sizeof(h));
+  }
+  return kSuccess;
+}
+
+int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* peers) {
+  if (!c || !peers || size < 1 || size > kMaxGroup || rank < 0 || rank >= size) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->fresh || c->npend || c->gsize > 1) return kInvalidResource;
+  CK(hipSetDevice(c->device));
+  if (size == 1) return kSuccess;
+  const pid_t me = getpid();
+  bool sys = false;
+  for (int i = 0; i < size; i++) {
+    const cairo_peer& p = peers[i];
+    if (p.width != c->w || p.height != c->h || p.ring != c->ring || p.stages < 2) return kInvalidArg;
+    if (i == rank) continue;
+    if (p.pid != me || p.device != c->device) sys = true;
+    if (p.device != c->device || p.pid != me) {
+      if (!p.fine_grained || !c->fine_grained) {
+        fprintf(stderr, "[cairo_amd] group members on other devices or processes need cairo_ctx_peer_info(..., 1)\n");
+        return kInvalidArg;
+      }
+    }
+  }
+  for (int i = 0; i < size; i++) {
+    cairo_ctx::Peer& q = c->gp[i];
+    const cairo_peer& p = peers[i];
+    q.stages = p.stages;
+    if (i == rank) {
+      q.ring = c->ring_buf, q.coef = c->coef, q.progress = c->progress;
+    } else if (p.pid == me) {  // same process: the addresses are valid here
+      if (p.device != c->device) {
+        const hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          c->gsize = i;
+          leave_group(c);
+          return fail(e, "hipDeviceEnablePeerAccess");
+        }
+      }
+      q.ring = (int16_t*)(uintptr_t)p.ring_addr;
+      q.coef = (int16_t*)(uintptr_t)p.coef_addr;
+      q.progress = (uint64_t*)(uintptr_t)p.progress_addr;
+    } else {  // another process: open its IPC handles (peer access over xGMI)
+      void* m[3] = {nullptr, nullptr, nullptr};
+      for (int k = 0; k < 3; k++) {
+        hipIpcMemHandle_t h;
+        memcpy(&h, p.ipc[k], sizeof(h));
+        const hipError_t e = hipIpcOpenMemHandle(&m[k], h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+          for (int j = 0; j < k; j++) (void)hipIpcCloseMemHandle(m[j]);
+          c->gsize = i;
+          leave_group(c);
+          return fail(e, "hipIpcOpenMemHandle");
+        }
+      }
+      q.ring = (int16_t*)m[0], q.coef = (int16_t*)m[1], q.progress = (uint64_t*)m[2];
+      q.imported = true;
+    }
+  }
+  c->gsize = size;
+  c->grank = rank;
+  c->gbase = c->next_ticket;
+  c->sys = sys;
+  CK(hipMalloc(&c->zero, c->plane_elems * 2));
+  CK(hipMemset(c->zero, 0, c->plane_elems * 2));
+  // a member's consecutive frames are N stream frames apart
+  const std::vector<int32_t> ord = task_order((int)c->hmb, 3 * size + 2);
+  CK(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  return kSuccess;
 }
 
 int cairo_ctx_release(cairo_ctx* c, int ticket) {

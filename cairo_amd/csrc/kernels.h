@@ -50,6 +50,8 @@ __host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
 
 // Frames per engine launch.
 constexpr int kMaxBatch = 32;
+// Members of a frame-interleaved group (cairo_ctx_join_group).
+constexpr int kMaxGroup = 16;
 
 // One frame of a batch (host-filled, kernarg).
 struct FrameDesc {
@@ -69,6 +71,7 @@ struct FrameDesc {
   PlaneSet coef_prev;        // the previous frame's output_cache (copy-macroblock chain)
   uint64_t* progress;        // this frame's deblock progress words [hmb]
   const uint64_t* prev_progress;  // the previous frame's (nullptr: none, first frame after a reset)
+  int sys;                   // FrameArgs::sys
   const BlockDesc* host_table;  // decode: the frame's block table and coefficient planes (y, u, v
   const int16_t* host_coef;     //   contiguous), uploaded at launch
 };
@@ -112,6 +115,11 @@ struct FrameArgs {
   // earlier frame is final there), so no launch ordering guards them.
   uint64_t* progress;             // [hmb] this frame's
   const uint64_t* prev_progress;  // [hmb] the previous frame's (nullptr: none)
+  // 1: the cross-frame buffers are shared with other devices or processes (a
+  // frame-interleaved group): progress words are stored and polled at system
+  // scope, with a system-scope release before each store and a system-scope
+  // acquire after each wait on another frame's data.
+  int sys;
   uint64_t* stamps;    // diagnostic (nullptr = off)
   uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, kIStamps stamps (see kernels.hip)
   const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)

@@ -158,6 +158,19 @@ __device__ __forceinline__ uint64_t tagged(uint32_t epoch, int cols) {
 __device__ __forceinline__ uint64_t progress_at(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The previous frame's words may live on another device (FrameArgs::sys).
+__device__ __forceinline__ uint64_t progress_peer(bool sys, const uint64_t* p) {
+  return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+             : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Acquire after a wait (thread 0): agent scope, or system scope when the data
+// released by the observed word may come from another device.
+__device__ __forceinline__ void acquire_fence(bool sys) {
+  if (sys)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
 
 // Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
 // timeout (~2 s) the error word is set and the wait gives up, so every
@@ -179,9 +192,9 @@ __device__ __forceinline__ void wait_at_least(int32_t* word, int target, int32_t
 
 // Consumer side of a hand-off: one lane waited; invalidate this CU's L1 and
 // let every wave load only after the barrier (MI355X_MICROARCH.md, Valid forms).
-__device__ __forceinline__ void acquire_after_wait() {
+__device__ __forceinline__ void acquire_after_wait(bool sys = false) {
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    acquire_fence(sys);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -666,7 +679,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int r, int rr, int need, DbLd
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
-      if (!a.prev_progress || progress_at(a.prev_progress + rr) >= tagged(a.epoch - 1, need)) {
+      if (!a.prev_progress || progress_peer(a.sys, a.prev_progress + rr) >= tagged(a.epoch - 1, need)) {
         d = 1;
       } else if (kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
         d = 2;
@@ -688,7 +701,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int r, int rr, int need, DbLd
     if (d == 2) deblock_chunk(a, r, D, st);
   }
   if (threadIdx.x == 0) {  // the check used a relaxed load: acquire what it observed
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    acquire_fence(a.sys);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -1201,7 +1214,14 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(&prog[r], above | (uint32_t)w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {
+        if (a.sys) {  // the next frame may read this row from another device
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          __hip_atomic_store(&prog[r], above | (uint32_t)w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+          __hip_atomic_store(&prog[r], above | (uint32_t)w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       if (a.stamps && tid == 0 && k < kDbStamps)
         a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps + k] = __builtin_amdgcn_s_memrealtime();
       w0 = w1;
@@ -1489,7 +1509,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
       if ((bx & 3) == 0) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
         if (tid == 0) wait_at_least(&a.inter_done[by * a.ng + (bx >> 2)], a.nref, err, a.sticky);
-        acquire_after_wait();
+        acquire_after_wait(a.sys);  // the stale rows, references and previous output_cache
       }
 
       // ---- window.  Reconstruction of the rows above arrives as granules
@@ -1974,6 +1994,7 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, a.ng, j);
   a.progress = f.progress;
   a.prev_progress = f.prev_progress;
+  a.sys = f.sys;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   {
     const int ng = (e.wmb + 3) / 4;

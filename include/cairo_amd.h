@@ -129,6 +129,40 @@ CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[4], int *frames);
  * one before it). */
 CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows);
 
+/* ---- frame-interleaved groups (multi-GPU single stream) ----
+ * N contexts (one per GPU and process, or several on one device) encode ONE
+ * stream: member k encodes the frames n = k (mod N), in order, reading the
+ * other members' reconstructions (references, the stale rows of frame n-R),
+ * output_cache (copy macroblocks) and deblock progress in place -- over xGMI
+ * when they live on other GPUs.  The hand-off is a per-row progress word; no
+ * collective and no copy is on the data path.  Output is the single-context
+ * stream, bit for bit.
+ *
+ * Protocol: create every member (same width, height, ring), call
+ * cairo_ctx_peer_info on each (cross_device = 1 if any member is another
+ * process or device: the shared buffers are then re-allocated fine-grained),
+ * exchange the records (any transport: they are plain bytes), then
+ * cairo_ctx_join_group on each with all N records in rank order, before any
+ * frame.  Submit frame n to member n % N with index n; before waiting on a
+ * frame, every member must have launched (cairo_ctx_flush) its frames that
+ * precede it in the stream -- a member's in-kernel wait on another's
+ * unlaunched frame times out after 2 s (EVX_ERROR_HARDWAREFAIL).  Members on
+ * one device share its workgroup slots: give each cairo_ctx_max_workgroups /
+ * (members on the device) row coders (cairo_ctx_set_workgroups).
+ * cairo_ctx_reset leaves the group. */
+typedef struct cairo_peer {
+  uint32_t width, height, ring;
+  int32_t device, pid, stages, fine_grained, reserved;
+  uint64_t ring_addr, coef_addr, progress_addr; /* device addresses in the owner's process */
+  uint8_t ipc[3][64];                           /* hipIpcMemHandle_t of the three buffers */
+} cairo_peer;
+CAIRO_API int cairo_ctx_peer_info(cairo_ctx *ctx, int cross_device, cairo_peer *out);
+CAIRO_API int cairo_ctx_join_group(cairo_ctx *ctx, int size, int rank, const cairo_peer *peers);
+/* Launch the pending (partial) batch now. */
+CAIRO_API int cairo_ctx_flush(cairo_ctx *ctx);
+/* Upper bound of cairo_ctx_set_workgroups on this device. */
+CAIRO_API int cairo_ctx_max_workgroups(const cairo_ctx *ctx);
+
 /* Known-answer check of the device transform chain: count macroblocks of 384
  * int16 (block-major: Y TL,TR,BL,BR, U, V; 64 each).  qtype[2m] = block type,
  * qtype[2m+1] = frame quality.  Host buffers in and out. */

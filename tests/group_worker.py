@@ -1,0 +1,117 @@
+"""Frame-interleaved group parity worker (run by tests/test_gpu_group.py in a
+subprocess, GPU test infrastructure).
+
+  inproc: N member contexts in this process on one device (the multi-GPU
+          protocol emulated on one GPU); this process needs
+          GPU_MAX_HW_QUEUES >= 3 N (each member's two launch streams and copy
+          stream on hardware queues of their own: a launch queued behind
+          another member's on a shared queue would wait for it).
+  xproc:  this process is member RANK of N processes on one device, sharing
+          its buffers through IPC handles (cross_device records: fine-grained
+          memory, system-scope hand-offs), records exchanged over gloo.
+
+Every frame's block table and coefficients and the final reconstructions are
+compared with the oracle encoding the same stream in one context.  Prints
+one JSON line; exit status 0 = bit-exact.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import cairo_amd  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+
+def table_mismatch(a, b):
+    return [f for f in a.dtype.names if f != "pad" and not np.array_equal(a[f], b[f])]
+
+
+def oracle_stream(w, h, ring, q, frames, intra_every):
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    ref = []
+    for t in range(frames):
+        intra = t == 0 or (intra_every and t % intra_every == 0)
+        if intra:
+            e.insert_intra()
+        e.encode(orc.make_frame(w, h, t))
+        ref.append((intra, e.block_table(), e.planes(1)))
+    final = {t: e.planes(2 + t % ring) for t in range(max(0, frames - ring), frames)}
+    return ref, final
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["inproc", "xproc"])
+    ap.add_argument("--members", type=int, default=2)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--store", default="")
+    ap.add_argument("--w", type=int, default=352)
+    ap.add_argument("--h", type=int, default=288)
+    ap.add_argument("--ring", type=int, default=4)
+    ap.add_argument("--q", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=12)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--intra-every", type=int, default=0)
+    a = ap.parse_args()
+    w, h, ring, q, F, N = a.w, a.h, a.ring, a.q, a.frames, a.members
+    ref, final = oracle_stream(w, h, ring, q, F, a.intra_every)
+    bad = []
+    if a.mode == "inproc":
+        g = cairo_amd.Group(w, h, ring, [0] * N, batch=a.batch)
+        assert F <= N * g.stages  # every frame in flight at once
+        for t in range(F):
+            g.submit(orc.make_frame(w, h, t), t, not ref[t][0], q)
+        for t in range(F):
+            out = g.wait(t)
+            if table_mismatch(out.table, ref[t][1]) or any(
+                    not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
+                bad.append(t)
+            g.release(t)
+        for t, planes in final.items():
+            if any(not np.array_equal(x, y) for x, y in zip(g.recon(t), planes)):
+                bad.append(f"recon {t}")
+        g.close()
+    else:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", init_method=f"file://{a.store}", rank=a.rank, world_size=N)
+        ctx = cairo_amd.Context(w, h, ring)
+        ctx.set_batch(a.batch)
+        ctx.set_workgroups(max(1, ctx.max_workgroups() // N))  # N members share the device
+        recs = [None] * N
+        dist.all_gather_object(recs, ctx.peer_info(cross_device=True))
+        ctx.join_group(a.rank, recs)
+        mine = [t for t in range(F) if t % N == a.rank]
+        frames = {t: orc.make_frame(w, h, t) for t in mine}
+        dist.barrier()  # every member ready: in-kernel waits on the others are bounded (2 s)
+        tk = {t: ctx.submit(frames[t], t, not ref[t][0], q) for t in mine}
+        ctx.flush()
+        for t in mine:
+            out = ctx.wait(tk[t])
+            if table_mismatch(out.table, ref[t][1]) or any(
+                    not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
+                bad.append(t)
+            ctx.release(tk[t])
+        S = -(-ring // N)
+        for t, planes in final.items():
+            if t % N == a.rank:
+                got = ctx.read_planes(2 + (t // N) % S)
+                if any(not np.array_equal(x, y) for x, y in zip(got, planes)):
+                    bad.append(f"recon {t}")
+        dist.barrier()  # the others may still read this member's buffers until they finish
+        ctx.close()
+        dist.destroy_process_group()
+    print(json.dumps({"mode": a.mode, "rank": a.rank, "members": N, "frames": F, "mismatched": bad}), flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
