@@ -23,8 +23,11 @@ Other legs (rank 0, N = 1), outside the timed region:
               host RGB in, bitstream out: the reference's own interface)
   cpu_baseline  the oracle (C restatement) on one host core, bounded sample
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank encodes its
-own stream (replicas, weak scaling: DESIGN.md §6), value = aggregate.
+Multi-GPU: one process per GPU (torch.distributed.run).  value: every rank
+encodes its own stream (replicas, weak scaling), the aggregate.  single_stream
+(N > 1): ONE stream over all ranks, frame-interleaved (rank k encodes frames
+n = k mod N, reading the others' reconstructions in place over xGMI; strong
+scaling over the same frames as N = 1), DESIGN.md §6.
 """
 from __future__ import annotations
 
@@ -72,6 +75,8 @@ def parse():
                    help="entropy workers per rank (0: min(14, host CPUs / ranks - 2); the GPU box gives 16 CPUs per GPU)")
     p.add_argument("--no-end-to-end", action="store_true")
     p.add_argument("--no-api", action="store_true")
+    p.add_argument("--no-single-stream", action="store_true",
+                   help="N > 1: skip the frame-interleaved single-stream leg")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
     p.add_argument("--batch", type=int, default=0, help="frames per engine launch (0 = library default)")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
@@ -180,9 +185,22 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
+    # Rehearsal of the multi-rank paths on a one-GPU box (tests, never the
+    # driver's runs): CAIRO_BENCH_SHARED_DEVICE=1 puts every rank on device 0,
+    # over gloo (RCCL refuses two ranks on one GPU), each with its share of
+    # the workgroup slots.
+    shared = world > 1 and os.environ.get("CAIRO_BENCH_SHARED_DEVICE") == "1"
+    if shared:
+        local = 0
+    if world > 1:
+        dist.init_process_group("gloo" if shared else "nccl")
     torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cpu") if shared else torch.device("cuda", local)
+
+    def share(c):  # ranks sharing one device split its resident workgroup slots
+        if shared:
+            c.set_workgroups(max(1, c.max_workgroups() // world))
+        return c
 
     import cairo_amd
 
@@ -204,7 +222,7 @@ def main():
     def frame_ptr(f):
         return base + f * stride
 
-    ctx = cairo_amd.Context(w, h, ring, device=local)
+    ctx = share(cairo_amd.Context(w, h, ring, device=local))
     ctx.set_batch(batch)
     if a.rows:
         ctx.set_workgroups(a.rows)
@@ -289,12 +307,16 @@ def main():
     e2e = None
     e2e_records = {}
     if not a.no_end_to_end:
-        ctx2 = cairo_amd.Context(w, h, ring, device=local)
+        ctx2 = share(cairo_amd.Context(w, h, ring, device=local))
         ctx2.set_batch(batch)
         e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, warm_frames, timed_frames, barrier, dist,
                          dev, world, n_check, e2e_records)
         ctx2.close()
     ctx.close()
+    single = None
+    if world > 1 and not a.no_single_stream:
+        single = single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm_frames, timed_frames, barrier,
+                               dist, dev, world, rank, local, share)
     del frames
     torch.cuda.empty_cache()
 
@@ -325,6 +347,7 @@ def main():
         "roofline_valu": valu,
         "end_to_end": e2e,
         "api_encode": api,
+        "single_stream": single,
     }
     if check:
         result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, n_check - 1,
@@ -335,6 +358,101 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, barrier, dist, dev, world, rank,
+                  local, share):
+    """N > 1: ONE stream over all ranks, frame-interleaved:
+    rank k encodes frames n = k (mod N), reading the other ranks'
+    reconstructions, output_cache and progress words in place over xGMI
+    (IPC handles exchanged over gloo).  Strong scaling: the same frames as
+    the N = 1 run, value = stream pixels / max-over-ranks time.  The first
+    frames are serialized and compared with the oracle on rank 0.  Failures
+    are reported, not raised (the replicas line above stays valid)."""
+    import torch
+
+    gloo = dist.new_group(backend="gloo")
+    res, err = None, ""
+    n_check = 4
+    recs = {}
+    ctx = None
+    try:
+        ctx = share(cairo_amd.Context(w, h, ring, device=local))
+        ctx.set_batch(batch)
+        peers = [None] * world
+        dist.all_gather_object(peers, ctx.peer_info(cross_device=True), group=gloo)
+        ctx.join_group(rank, peers)
+        stages = ctx.stages
+
+        def run(first, count, keep):
+            inflight = deque()
+
+            def retire():
+                n, t = inflight.popleft()
+                out = ctx.wait(t, copy=False)
+                if keep and n < n_check:
+                    data, nbits = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, out.coef_y, out.coef_u,
+                                                            out.coef_v)
+                    recs[n] = record(cairo_amd, w, h, ring, q, n, data, nbits)
+                ctx.release(t)
+
+            for n in range(first, first + count):
+                if n % world != rank:
+                    continue
+                if len(inflight) == stages:
+                    retire()
+                inflight.append((n, ctx.submit(frame_ptr(n), n, n > 0, q, on_device=True)))
+            ctx.flush()
+            while inflight:
+                retire()
+
+        dist.barrier(group=gloo)  # in-kernel waits on other ranks' frames are bounded (2 s): start together
+        run(0, warm, True)
+        ctx.sync()
+        dist.barrier(group=gloo)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(warm, timed, False)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        dist.barrier(group=gloo)
+        res = el
+    except Exception as ex:  # noqa: BLE001 -- reported in the line
+        err = f"rank {rank}: {type(ex).__name__}: {ex}"[:300]
+    ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=gloo)
+    elt = torch.tensor([res or 0.0], dtype=torch.float64)
+    dist.all_reduce(elt, op=dist.ReduceOp.MAX, group=gloo)
+    errs = [None] * world
+    dist.all_gather_object(errs, err, group=gloo)
+    allrecs = [None] * world
+    dist.all_gather_object(allrecs, recs, group=gloo)
+    dist.barrier(group=gloo)  # nobody frees buffers another rank may still read
+    if ctx is not None:
+        ctx.close()
+    if ok.item() < 1:
+        return {"error": [e for e in errs if e]}
+    el = float(elt.item())
+    out = {"value": round(aggregate_mpix(w, h, timed, 1, el), 3), "unit": "Mpix/s", "scaling": "strong",
+           "members": world, "ms_per_frame": round(el * 1e3 / timed, 4), "timed_frames": timed,
+           "note": "one stream, frame n on rank n % N (frame-interleaved group, in-place reads over xGMI); same "
+                   "frames as the N = 1 run"}
+    if rank == 0:
+        from oracle import oracle as orc
+
+        got = {}
+        for r in allrecs:
+            got.update(r)
+        e = orc.OracleEncoder(ring)
+        e.set_quality(q)
+        mism = []
+        for t in range(n_check):
+            data, nb = e.encode(cairo_amd.make_band4(w, h, t))
+            if t not in got or orc.canonical_frame_bytes(got[t][0], got[t][1], t == 0) != \
+                    orc.canonical_frame_bytes(data, nb, t == 0):
+                mism.append(t)
+        out["bit_exact"] = {"frames_checked": n_check, "mismatched_frames": mism, "bit_exact": not mism}
+    return out
 
 
 def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier, dist, dev, world, n_check,
