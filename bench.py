@@ -195,7 +195,7 @@ def main():
     if world > 1:
         dist.init_process_group("gloo" if shared else "nccl")
     torch.cuda.set_device(local)
-    dev = torch.device("cpu") if shared else torch.device("cuda", local)
+    dev = torch.device("cpu") if shared else torch.device("cuda", local)  # where collectives' tensors live
 
     def share(c):  # ranks sharing one device split its resident workgroup slots
         if shared:
@@ -209,7 +209,7 @@ def main():
     warm_frames, timed_frames = a.warmup * batch, a.steps * batch
     nframes = warm_frames + timed_frames
     # synthetic input, generated on host threads and uploaded to HBM before timing
-    frames = torch.empty((nframes, h, w, 3), dtype=torch.uint8, device=dev)
+    frames = torch.empty((nframes, h, w, 3), dtype=torch.uint8, device=torch.device("cuda", local))
     chunk = 16
     with ThreadPoolExecutor(max(1, min(8, host_cpus()))) as pool:
         for c0 in range(0, nframes, chunk):

@@ -279,6 +279,10 @@ int zero_state(cairo_ctx* c) {
   CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2 * S, c->ks));
   CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
   CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * S, c->ks));
+  // inter records: a frame whose search was cut short by a timed-out wait
+  // still reads in-frame motion vectors
+  CK(hipMemsetAsync(c->idesc, 0, c->nref * c->mbs * sizeof(BlockDesc) * S, c->ks));
+  CK(hipMemsetAsync(c->isad, 0, c->nref * c->mbs * sizeof(int32_t) * S, c->ks));
   // granule tags start at 0; the n-th submission after a reset publishes tag n
   CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * S, c->ks));
   CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t) * kSyncAreas, c->ks));
@@ -653,6 +657,15 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   if (s.busy) {
     fprintf(stderr, "[cairo_amd] staging slot of ticket %d not released\n", s.ticket);
     return kInvalidResource;
+  }
+  if (rgb_on_device) {  // the kernels read it: it must be device memory of this context's GPU
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, rgb) != hipSuccess || pa.type != hipMemoryTypeDevice || pa.device != c->device) {
+      (void)hipGetLastError();
+      fprintf(stderr, "[cairo_amd] submit: rgb_on_device but %p is not device memory of device %d\n", (const void*)rgb,
+              c->device);
+      return kInvalidArg;
+    }
   }
   FrameDesc& f = c->pend[c->npend];
   if (rgb_on_device) {

@@ -229,3 +229,16 @@ def test_sync_encoder_memory_4k(cairo):
     enc.close()
     used = free0 - free1
     assert used < 1 << 30, f"{used / 2**20:.0f} MiB"
+
+
+def test_submit_rejects_host_pointer_as_device(cairo):
+    """rgb_on_device with a host address is refused before any kernel reads
+    it (a device-side read of it would fault the GPU)."""
+    w, h = 352, 288
+    ctx = cairo.Context(w, h, 2)
+    rgb = cairo.make_band4(w, h, 0)
+    with pytest.raises(cairo.CairoError):
+        ctx.submit(rgb.ctypes.data, 0, False, 16, on_device=True)
+    out = ctx.encode_frame(rgb, 0, False, 16)  # the context is still usable
+    assert out.table.size == ctx.wmb * ctx.hmb
+    ctx.close()
