@@ -11,7 +11,7 @@ LIB      = cairo_amd/_lib/libcairo_amd.so
 ORACLE   = oracle/liboracle.so
 API_BIN  = cairo_amd/_lib/evx1_api_caller
 
-HIP_SRCS = $(SRC)/kernels.hip $(SRC)/backend.hip
+HIP_SRCS = $(SRC)/kernels.hip $(SRC)/backend.hip $(SRC)/precode.hip
 CPP_SRCS = $(SRC)/entropy.cpp $(SRC)/bitstream.cpp $(SRC)/encoder.cpp $(SRC)/decoder.cpp $(SRC)/pipeline.cpp $(SRC)/unserialize.cpp
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
 HDRS     = $(wildcard $(SRC)/*.h) $(wildcard include/*.h)

@@ -36,6 +36,8 @@ BLOCK_DESC = np.dtype(
 assert BLOCK_DESC.itemsize == 16
 
 EVX_SUCCESS = 0
+OUT_COEF, OUT_FEED = 1, 2  # cairo_ctx_set_outputs
+FEED_NONE, FEED_VALID, FEED_OVERFLOW = 0, 1, 2
 PEER_SIZE = 3 * 4 + 5 * 4 + 3 * 8 + 3 * 64  # sizeof(cairo_peer)
 # EVX_PEEK_STATE (reference evx1.h:55-64)
 PEEK_SOURCE, PEEK_PREDICTION, PEEK_BLOCK_TABLE, PEEK_QUANT_TABLE, PEEK_SPMP_TABLE, PEEK_BLOCK_VARIANCE, \
@@ -91,6 +93,9 @@ def lib() -> ctypes.CDLL:
         "cairo_default_batch": (I, [U, U]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
+        "cairo_serialize_feed": (I, [P, ctypes.c_uint64, P, U, ctypes.POINTER(U)]),
+        "cairo_ctx_set_outputs": (I, [P, I]),
+        "cairo_ctx_fetch_coef": (I, [P, I, P]),
         "cairo_unserialize_slice": (I, [P, ctypes.POINTER(U), U, U, U, U, P, P, P, P]),
         "cairo_stream_create": (I, [P, I, ctypes.POINTER(P)]),
         "cairo_stream_submit": (I, [P, P, I, U, U, U, ctypes.POINTER(I)]),
@@ -174,6 +179,9 @@ class _FrameResult(ctypes.Structure):
         ("index", ctypes.c_uint32),
         ("type", ctypes.c_uint32),
         ("quality", ctypes.c_uint32),
+        ("feed", ctypes.c_void_p),
+        ("feed_bits", ctypes.c_uint64),
+        ("feed_status", ctypes.c_int32),
     ]
 
 
@@ -182,9 +190,12 @@ class FrameOutputs:
     """Host copies of one frame's outputs (block table + output_cache)."""
 
     table: np.ndarray  # (mbs,) BLOCK_DESC
-    coef_y: np.ndarray
-    coef_u: np.ndarray
-    coef_v: np.ndarray
+    coef_y: np.ndarray | None  # None without OUT_COEF (Context.fetch_coef)
+    coef_u: np.ndarray | None
+    coef_v: np.ndarray | None
+    feed: np.ndarray | None = None  # OUT_FEED: the GPU precode's feed words (uint32, LSB-first)
+    feed_bits: int = 0
+    feed_status: int = 0  # FEED_NONE / FEED_VALID / FEED_OVERFLOW
 
 
 def _view(addr: int, dtype, count: int) -> np.ndarray:
@@ -235,17 +246,38 @@ class Context:
         r = _FrameResult()
         _ck(self.L.cairo_ctx_wait(self.h, ticket, ctypes.byref(r)), "cairo_ctx_wait")
         self._keep.pop(ticket, None)
+        return self._outputs(r, copy)
+
+    def _outputs(self, r, copy: bool) -> FrameOutputs:
         ny, nc = r.wa * r.ha, (r.wa // 2) * (r.ha // 2)
         mbs = r.wmb * r.hmb
+        has_coef = bool(r.coef_y)
+        feed = _view(r.feed, np.uint32, (r.feed_bits + 31) // 32) if r.feed_status == FEED_VALID else None
         out = FrameOutputs(
             _view(r.block_table, BLOCK_DESC, mbs),
-            _view(r.coef_y, np.int16, ny).reshape(r.ha, r.wa),
-            _view(r.coef_u, np.int16, nc).reshape(r.ha // 2, r.wa // 2),
-            _view(r.coef_v, np.int16, nc).reshape(r.ha // 2, r.wa // 2),
+            _view(r.coef_y, np.int16, ny).reshape(r.ha, r.wa) if has_coef else None,
+            _view(r.coef_u, np.int16, nc).reshape(r.ha // 2, r.wa // 2) if has_coef else None,
+            _view(r.coef_v, np.int16, nc).reshape(r.ha // 2, r.wa // 2) if has_coef else None,
+            feed, int(r.feed_bits), int(r.feed_status),
         )
         if copy:
-            out = FrameOutputs(*(a.copy() for a in (out.table, out.coef_y, out.coef_u, out.coef_v)))
+            cp = lambda a: None if a is None else a.copy()  # noqa: E731
+            out = FrameOutputs(cp(out.table), cp(out.coef_y), cp(out.coef_u), cp(out.coef_v), cp(out.feed),
+                               out.feed_bits, out.feed_status)
         return out
+
+    def set_outputs(self, outputs: int) -> None:
+        """OUT_COEF and/or OUT_FEED for frames submitted from now on."""
+        _ck(self.L.cairo_ctx_set_outputs(self.h, outputs), "cairo_ctx_set_outputs")
+
+    def fetch_coef(self, ticket: int):
+        """(y, u, v) output_cache planes of a waited, unreleased frame (copies)."""
+        r = _FrameResult()
+        _ck(self.L.cairo_ctx_fetch_coef(self.h, ticket, ctypes.byref(r)), "cairo_ctx_fetch_coef")
+        ny, nc = self.wa * self.ha, (self.wa // 2) * (self.ha // 2)
+        return (_view(r.coef_y, np.int16, ny).reshape(self.ha, self.wa).copy(),
+                _view(r.coef_u, np.int16, nc).reshape(self.ha // 2, self.wa // 2).copy(),
+                _view(r.coef_v, np.int16, nc).reshape(self.ha // 2, self.wa // 2).copy())
 
     def release(self, ticket: int) -> None:
         _ck(self.L.cairo_ctx_release(self.h, ticket), "cairo_ctx_release")
@@ -419,6 +451,16 @@ def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv
     )
     n = pos.value
     return out[: (n + 7) // 8].tobytes(), n
+
+
+def serialize_feed(feed: np.ndarray, feed_bits: int, capacity_bytes: int | None = None):
+    """The arithmetic coder over a GPU-precoded feed (FrameOutputs.feed) -> (bytes, nbits)."""
+    cap = capacity_bytes or (feed_bits // 8 * 2 + 65536)
+    out = np.empty(cap, np.uint8)
+    pos = ctypes.c_uint32(0)
+    f = np.ascontiguousarray(feed, dtype=np.uint32)
+    _ck(lib().cairo_serialize_feed(_ptr(f), feed_bits, _ptr(out), cap, ctypes.byref(pos)), "cairo_serialize_feed")
+    return out[: (pos.value + 7) // 8].tobytes(), pos.value
 
 
 def unserialize_slice(payload: bytes, nbits: int, wmb: int, hmb: int, ring: int, table=None, planes=None,

@@ -31,6 +31,7 @@
 #include "../../include/cairo_amd.h"
 #include "ctx_internal.h"
 #include "kernels.h"
+#include "precode.h"
 
 using namespace cairo;
 
@@ -121,6 +122,16 @@ struct cairo_ctx {
   Peer gp[kMaxGroup];
   int16_t* zero = nullptr;  // a zero plane set: references before the stream start
   bool fine_grained = false;  // ring / coef / progress allocated fine-grained (cross-device sharing)
+  // Outputs for the host entropy stage (cairo_ctx_set_outputs): the
+  // coefficient planes (D2H per frame) and/or the GPU precode's feed bits
+  // (precode.hip), written straight into mapped pinned host memory.
+  int outputs = CAIRO_OUT_COEF;
+  size_t feed_words = 0;          // per staging slot
+  uint32_t* feed_dev = nullptr;   // [stages][feed_words]
+  uint32_t* feed_hdr = nullptr;   // [stages][kFeedHdrWords]
+  int32_t* feed_lens = nullptr;   // [stages][6 * mbs]
+  uint32_t* feed_host = nullptr;  // mapped pinned [stages][kFeedHdrWords + feed_words]
+  hipStream_t fs = nullptr;       // synchronous coefficient fetches (a frame whose feed overflowed)
   bool sys = false;           // a member is another process or device: system-scope hand-offs
   int32_t *sync = nullptr, *sticky = nullptr;
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
@@ -258,9 +269,11 @@ void free_ctx(cairo_ctx* c) {
   for (auto& ev : c->batch_end)
     if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
+  if (c->feed_host) (void)hipHostFree(c->feed_host);
+  if (c->fs) (void)hipStreamDestroy(c->fs);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
   leave_group(c);
-  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress,
+  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress, (void*)c->feed_dev, (void*)c->feed_hdr, (void*)c->feed_lens,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps})
     (void)hipFree(p);
@@ -389,6 +402,22 @@ int flush(cairo_ctx* c) {
   }
   const int last = c->pend[e.nframes - 1].slot;
   if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
+  if (c->outputs & CAIRO_OUT_FEED) {  // the entropy precode, straight into mapped host memory
+    FeedArgs fa;
+    memset(&fa, 0, sizeof(fa));
+    fa.nframes = e.nframes;
+    fa.fa = fd;
+    for (int i = 0; i < e.nframes; i++) {
+      fa.slot[i] = c->pend[i].slot;
+      fa.host[i] = c->feed_host + (size_t)fa.slot[i] * (kFeedHdrWords + c->feed_words);
+    }
+    fa.lens = c->feed_lens;
+    fa.lens_stride = 6 * c->mbs;
+    fa.feed = c->feed_dev;
+    fa.feed_stride = c->feed_words;
+    fa.hdr = c->feed_hdr;
+    CK(launch_precode(fa, (int)c->mbs, st));
+  }
   // outputs for the host entropy stage, on the copy stream
   CK(hipEventRecord(c->batch_end[area], st));
   CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
@@ -401,8 +430,9 @@ int flush(cairo_ctx* c) {
     }
     CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
                       hipMemcpyDeviceToHost, c->cs));
-    CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2,
-                      hipMemcpyDeviceToHost, c->cs));
+    if (c->outputs & CAIRO_OUT_COEF)
+      CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2,
+                        hipMemcpyDeviceToHost, c->cs));
     CK(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
     CK(hipEventRecord(s.d2h_done, c->cs));
     s.launched = true;
@@ -725,9 +755,23 @@ static int frame_result(cairo_ctx* c, Stage& s, cairo_frame_result* out, bool po
     return kHardwareFail;
   }
   out->block_table = s.table;
-  out->coef_y = s.coef;
-  out->coef_u = s.coef + (size_t)c->wa * c->ha;
-  out->coef_v = out->coef_u + (size_t)(c->wa / 2) * (c->ha / 2);
+  if (c->outputs & CAIRO_OUT_COEF) {
+    out->coef_y = s.coef;
+    out->coef_u = s.coef + (size_t)c->wa * c->ha;
+    out->coef_v = out->coef_u + (size_t)(c->wa / 2) * (c->ha / 2);
+  } else {
+    out->coef_y = out->coef_u = out->coef_v = nullptr;
+  }
+  out->feed = nullptr;
+  out->feed_bits = 0;
+  out->feed_status = CAIRO_FEED_NONE;
+  if (c->outputs & CAIRO_OUT_FEED) {
+    const int slot = (int)(&s - c->st.data());
+    const volatile uint32_t* h = c->feed_host + (size_t)slot * (kFeedHdrWords + c->feed_words);
+    out->feed = (const uint32_t*)h + kFeedHdrWords;
+    out->feed_bits = (uint64_t)h[0] | ((uint64_t)h[1] << 32);
+    out->feed_status = h[2] ? CAIRO_FEED_OVERFLOW : CAIRO_FEED_VALID;
+  }
   out->wa = c->wa;
   out->ha = c->ha;
   out->wmb = c->wmb;
@@ -808,6 +852,49 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
 }
 
 int cairo_ctx_max_workgroups(const cairo_ctx* c) { return c ? c->max_rows : 0; }
+
+int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
+  if (!c || outputs < 1 || outputs > (CAIRO_OUT_COEF | CAIRO_OUT_FEED)) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  CK(hipSetDevice(c->device));
+  int r = sync_all(c);  // frames in flight keep the outputs they were launched with
+  if (r) return r;
+  for (const Stage& s : c->st)
+    if (s.busy) return kInvalidResource;
+  if ((outputs & CAIRO_OUT_FEED) && !c->feed_dev) {
+    const size_t S = (size_t)c->stages;
+    c->feed_words = feed_words_per_slot(c->mbs);
+    CK(hipMalloc(&c->feed_dev, c->feed_words * 4 * S));
+    CK(hipMalloc(&c->feed_hdr, kFeedHdrWords * 4 * S));
+    CK(hipMalloc(&c->feed_lens, 6 * c->mbs * 4 * S));
+    CK(hipHostMalloc(&c->feed_host, (kFeedHdrWords + c->feed_words) * 4 * S, hipHostMallocMapped));
+    CK(hipStreamCreateWithFlags(&c->fs, hipStreamNonBlocking));
+  }
+  c->outputs = outputs;
+  return kSuccess;
+}
+
+int cairo_ctx_fetch_coef(cairo_ctx* c, int ticket, cairo_frame_result* out) {
+  if (!c || !out || ticket < 0) return kInvalidArg;
+  Stage& s = c->st[ticket % c->stages];
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!s.busy || s.ticket != ticket || !s.launched) return kInvalidResource;
+  }
+  CK(hipSetDevice(c->device));
+  CK(hipEventSynchronize(s.d2h_done));  // the frame's engine launch has finished
+  const int slot = ticket % c->stages;
+  if (!(c->outputs & CAIRO_OUT_COEF)) {  // still in the staging slot until its release
+    hipStream_t fs = c->fs ? c->fs : c->cs;
+    CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2, hipMemcpyDeviceToHost,
+                      fs));
+    CK(hipStreamSynchronize(fs));
+  }
+  out->coef_y = s.coef;
+  out->coef_u = s.coef + (size_t)c->wa * c->ha;
+  out->coef_v = out->coef_u + (size_t)(c->wa / 2) * (c->ha / 2);
+  return kSuccess;
+}
 
 int cairo_ctx_flush(cairo_ctx* c) {
   if (!c) return kInvalidArg;

@@ -3,8 +3,9 @@
 //
 // encode(): lazy init (header), frame descriptor, GPU hot path
 // (cairo_ctx_submit/wait: convert, inter + intra search, transform, VAQ,
-// quantize, reconstruct, deblock), host entropy (serialize_slice) appended to
-// the caller's bit_stream, then the reference's frame-state update.
+// quantize, reconstruct, deblock, and the entropy precode), the arithmetic
+// coder on the host appended to the caller's bit_stream, then the
+// reference's frame-state update.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -91,8 +92,7 @@ class gpu_encoder : public evx1_encoder {
       return EVX_ERROR_EXECUTION_FAILURE;
     }
     uint64_t pos = output->query_write_index();
-    r = cairo::serialize_slice(res.block_table, res.wmb, res.hmb, ring_, res.coef_y, res.coef_u,
-                               res.coef_v, output->query_data(), output->query_capacity(), &pos);
+    r = cairo::serialize_result(ctx_, ticket, &res, ring_, output->query_data(), output->query_capacity(), &pos);
     memcpy(last_table_, res.block_table, (size_t)res.wmb * res.hmb * 16);
     cairo_ctx_release(ctx_, ticket);
     if (r) return EVX_ERROR_EXECUTION_FAILURE;
@@ -192,6 +192,8 @@ class gpu_encoder : public evx1_encoder {
     // one frame in flight: two staging slots (the previous frame's output_cache
     // stays in the other one, for the copy-macroblock chain)
     if (cairo_ctx_create_ex(width, height, ring_, device_, 2, &ctx_)) return EVX_ERROR_HARDWAREFAIL;
+    // the GPU precodes the entropy feed; only the arithmetic coder runs here
+    if (cairo_ctx_set_outputs(ctx_, CAIRO_OUT_FEED)) return EVX_ERROR_HARDWAREFAIL;
     const size_t mbs = (size_t)((width + 15) / 16) * ((height + 15) / 16);
     last_table_ = (uint8 *)calloc(mbs, 16);
     if (!last_table_) return EVX_ERROR_OUTOFMEMORY;

@@ -275,6 +275,65 @@ void plane_blocks(Feed& f, const int16_t* img, uint32_t width, uint32_t height, 
 
 }  // namespace
 
+namespace {
+
+// Code nbits of feed into out at *bit_pos (bits of the first byte below it
+// preserved, bits beyond the end untouched).
+int code_feed(const uint64_t* feed, uint64_t nbits, uint8_t* out, uint64_t out_bits_capacity, uint64_t* bit_pos) {
+  const uint64_t pos0 = *bit_pos;
+  if (pos0 > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
+  // Code the feed into scratch (bit 0 = bit 0 of the caller's byte pos0 / 8,
+  // with its bits below pos0 preloaded), then copy; bits beyond the end stay
+  // untouched.
+  const uint64_t byte0 = pos0 >> 3, cap_bytes = (out_bits_capacity + 7) / 8 - byte0;
+  constexpr uint64_t kSlack = 512;  // > the output of one 64-symbol feed word
+  thread_local std::vector<uint8_t> scratch;
+  if (scratch.size() < cap_bytes + kSlack) scratch.resize(cap_bytes + kSlack);
+  uint8_t* const buf = scratch.data();
+  const uint32_t s0 = (uint32_t)(pos0 & 7);
+  const uint64_t total = abac_encode(feed, nbits, s0 ? out[byte0] : 0, s0, buf, buf + cap_bytes);
+  if (total == ~0ull || byte0 * 8 + total > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
+  const uint64_t n = total - s0;
+  const size_t whole = (size_t)(total >> 3);
+  memcpy(out + byte0, buf, whole);
+  if (total & 7) {
+    const uint8_t mask = (uint8_t)((1u << (total & 7)) - 1u);
+    out[byte0 + whole] = (uint8_t)((out[byte0 + whole] & ~mask) | (buf[whole] & mask));
+  }
+  *bit_pos = pos0 + n;
+  return 0;
+}
+
+}  // namespace
+
+int serialize_feed(const uint32_t* feed, uint64_t feed_bits, uint8_t* out, uint64_t out_bits_capacity,
+                   uint64_t* bit_pos) {
+  // the 32-bit feed words, LSB-first, are the coder's 64-bit words on a
+  // little-endian host; bits of the last word beyond feed_bits (the buffer
+  // has slack) are never coded
+  thread_local std::vector<uint64_t> words;
+  const size_t n64 = (size_t)((feed_bits + 63) / 64);
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(feed);
+  if ((uintptr_t)feed & 7) {  // unaligned: copy
+    words.assign(n64, 0);
+    memcpy(words.data(), feed, (size_t)((feed_bits + 31) / 32) * 4);
+    w = words.data();
+  }
+  return code_feed(w, feed_bits, out, out_bits_capacity, bit_pos);
+}
+
+int serialize_result(cairo_ctx* ctx, int ticket, cairo_frame_result* res, uint32_t ring, uint8_t* out,
+                     uint64_t out_bits_capacity, uint64_t* bit_pos) {
+  if (res->feed_status == CAIRO_FEED_VALID)
+    return serialize_feed(res->feed, res->feed_bits, out, out_bits_capacity, bit_pos);
+  if (!res->coef_y) {
+    const int r = cairo_ctx_fetch_coef(ctx, ticket, res);
+    if (r) return r;
+  }
+  return serialize_slice(res->block_table, res->wmb, res->hmb, ring, res->coef_y, res->coef_u, res->coef_v, out,
+                         out_bits_capacity, bit_pos);
+}
+
 int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t ring,
                     const int16_t* cy, const int16_t* cu, const int16_t* cv, uint8_t* out,
                     uint64_t out_bits_capacity, uint64_t* bit_pos) {
@@ -340,30 +399,19 @@ int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t r
   plane_blocks(f, cv, wa / 2, ha / 2, 8, table);
 
   f.close();
-
-  // Code the feed into scratch (bit 0 = bit 0 of the caller's byte pos0 / 8,
-  // with its bits below pos0 preloaded), then copy; bits beyond the end stay
-  // untouched.
-  const uint64_t byte0 = pos0 >> 3, cap_bytes = (out_bits_capacity + 7) / 8 - byte0;
-  constexpr uint64_t kSlack = 512;  // > the output of one 64-symbol feed word
-  thread_local std::vector<uint8_t> scratch;
-  if (scratch.size() < cap_bytes + kSlack) scratch.resize(cap_bytes + kSlack);
-  uint8_t* const buf = scratch.data();
-  const uint32_t s0 = (uint32_t)(pos0 & 7);
-  const uint64_t total = abac_encode(feed_words.data(), f.nbits, s0 ? out[byte0] : 0, s0, buf, buf + cap_bytes);
-  if (total == ~0ull || byte0 * 8 + total > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
-  const uint64_t nbits = total - s0;
-  const size_t whole = (size_t)(total >> 3);
-  memcpy(out + byte0, buf, whole);
-  if (total & 7) {
-    const uint8_t mask = (uint8_t)((1u << (total & 7)) - 1u);
-    out[byte0 + whole] = (uint8_t)((out[byte0 + whole] & ~mask) | (buf[whole] & mask));
-  }
-  *bit_pos = pos0 + nbits;
-  return 0;
+  return code_feed(feed_words.data(), f.nbits, out, out_bits_capacity, bit_pos);
 }
 
 }  // namespace cairo
+
+extern "C" int cairo_serialize_feed(const uint32_t* feed, uint64_t feed_bits, uint8_t* out, uint32_t out_bytes,
+                                    uint32_t* bit_pos) {
+  if (!feed || !out || !bit_pos) return 1;
+  uint64_t pos = *bit_pos;
+  int r = cairo::serialize_feed(feed, feed_bits, out, (uint64_t)out_bytes * 8u, &pos);
+  *bit_pos = (uint32_t)pos;
+  return r;
+}
 
 extern "C" int cairo_serialize_slice(const uint8_t* block_table, uint32_t wmb, uint32_t hmb,
                                      uint32_t ring, const int16_t* cy, const int16_t* cu,

@@ -13,8 +13,9 @@
 //
 //   caller thread     cairo_stream_submit  -> cairo_ctx_submit (launches full batches)
 //   completion thread waits for each frame's D2H (in ticket order) -> job queue
-//   entropy workers   serialize_slice into the frame's payload buffer,
-//                     release the staging slot
+//   entropy workers   the arithmetic coder over the frame's GPU-precoded feed
+//                     (serialize_slice from the planes if the feed overflowed)
+//                     into its payload buffer, release the staging slot
 //   caller thread     cairo_stream_collect -> payload bits appended in place
 //
 // Payload bits are the exact serialize_slice output of the frame, so
@@ -131,7 +132,7 @@ struct cairo_stream {
       }
       Frame& f = at(j.ticket);  // owned by this worker until kDone
       f.t[kTEntropy0] = now_us();
-      const cairo_frame_result& o = j.res;
+      cairo_frame_result& o = j.res;
       if (f.bits.empty()) f.bits.resize(std::max<size_t>((size_t)o.wa * o.ha / 2, 1 << 16));
       uint64_t pos = 0;
       int r;
@@ -141,8 +142,7 @@ struct cairo_stream {
           r = kSuccess;
           break;
         }
-        r = cairo::serialize_slice(o.block_table, wmb, hmb, ring, o.coef_y, o.coef_u, o.coef_v,
-                                   f.bits.data(), (uint64_t)f.bits.size() * 8, &pos);
+        r = cairo::serialize_result(ctx, j.ticket, &j.res, ring, f.bits.data(), (uint64_t)f.bits.size() * 8, &pos);
         // a frame's precode is bounded by the feed capacity per section, so
         // the payload is too; grow until it fits
         if (r != kCapacityLimit || f.bits.size() >= ((size_t)1 << 31)) break;
@@ -205,6 +205,13 @@ int cairo_stream_create(cairo_ctx* ctx, int threads, cairo_stream** out) {
   if (!s) return 3;
   s->ctx = ctx;
   s->stages = cairo_ctx_stages(ctx);
+  // the GPU precodes each frame's entropy feed; the workers run only the
+  // arithmetic coder
+  int ro = cairo_ctx_set_outputs(ctx, CAIRO_OUT_FEED);
+  if (ro) {
+    delete s;
+    return ro;
+  }
   int r = cairo::ctx_geometry(ctx, &s->wmb, &s->hmb, &s->ring, &s->next);
   if (r) {
     delete s;

@@ -34,14 +34,26 @@ extern "C" {
 
 typedef struct cairo_ctx cairo_ctx;
 
+/* Outputs a context hands to the host entropy stage (cairo_ctx_set_outputs). */
+#define CAIRO_OUT_COEF 1 /* the output_cache planes (default)                   */
+#define CAIRO_OUT_FEED 2 /* the GPU entropy precode: the exact feed bits the    */
+                         /* reference's coder consumes    */
+#define CAIRO_FEED_NONE 0
+#define CAIRO_FEED_VALID 1
+#define CAIRO_FEED_OVERFLOW 2 /* a coefficient section exceeds the reference's   */
+                              /* 32 Mbit feed stream: code it from the planes */
+
 /* Host-visible outputs of one frame; valid until cairo_ctx_release(ticket). */
 typedef struct cairo_frame_result {
   const uint8_t *block_table; /* wmb*hmb evx_block_desc (16 B, pack(2) layout) */
-  const int16_t *coef_y;      /* output_cache Y, wa x ha, pitch wa            */
-  const int16_t *coef_u;      /* output_cache U, wa/2 x ha/2, pitch wa/2      */
+  const int16_t *coef_y;      /* output_cache Y, wa x ha, pitch wa (NULL      */
+  const int16_t *coef_u;      /*   without CAIRO_OUT_COEF: cairo_ctx_fetch_coef) */
   const int16_t *coef_v;      /* output_cache V                               */
   uint32_t wa, ha, wmb, hmb;
   uint32_t index, type, quality;
+  const uint32_t *feed;       /* CAIRO_OUT_FEED: feed bits, LSB-first words   */
+  uint64_t feed_bits;
+  int32_t feed_status;        /* CAIRO_FEED_*                                 */
 } cairo_frame_result;
 
 /* Context = one encoder's device state: R ring slots, input and output_cache
@@ -160,6 +172,12 @@ CAIRO_API int cairo_ctx_peer_info(cairo_ctx *ctx, int cross_device, cairo_peer *
 CAIRO_API int cairo_ctx_join_group(cairo_ctx *ctx, int size, int rank, const cairo_peer *peers);
 /* Launch the pending (partial) batch now. */
 CAIRO_API int cairo_ctx_flush(cairo_ctx *ctx);
+/* Choose the outputs (CAIRO_OUT_COEF and/or CAIRO_OUT_FEED) for frames
+ * submitted from now on; no frame may be in flight. */
+CAIRO_API int cairo_ctx_set_outputs(cairo_ctx *ctx, int outputs);
+/* The coefficient planes of a waited, unreleased frame (a D2H copy from its
+ * staging slot when the context does not copy them already). */
+CAIRO_API int cairo_ctx_fetch_coef(cairo_ctx *ctx, int ticket, cairo_frame_result *out);
 /* Upper bound of cairo_ctx_set_workgroups on this device. */
 CAIRO_API int cairo_ctx_max_workgroups(const cairo_ctx *ctx);
 
@@ -177,6 +195,11 @@ CAIRO_API int cairo_serialize_slice(const uint8_t *block_table, uint32_t wmb, ui
                                     uint32_t ring, const int16_t *coef_y, const int16_t *coef_u,
                                     const int16_t *coef_v, uint8_t *out, uint32_t out_bytes,
                                     uint32_t *bit_pos);
+
+/* The same payload from a frame's GPU-precoded feed (cairo_frame_result.feed
+ * with CAIRO_FEED_VALID): only the arithmetic coder runs. */
+CAIRO_API int cairo_serialize_feed(const uint32_t *feed, uint64_t feed_bits, uint8_t *out,
+                                   uint32_t out_bytes, uint32_t *bit_pos);
 
 /* ---- host entropy decode (unserialize_slice, unserialize.cpp:321-342) ----
  * Decodes the ABAC payload of one frame starting at bit *read_index of data
