@@ -8,9 +8,9 @@ ring R = 4 (3 inter references), quality 16, band4 synthetic content
 A step = one engine launch's batch of P-frames (the library's default frames
 per launch for the frame size: 16 at 4K, 12 at 1080p, 32 at 720p) through the
 hot path: RGB->YUV, inter search, the macroblock wavefront (intra search,
-classify, transform, VAQ, quantize, reconstruct, in-loop deblock), and each
-frame's block table + coefficients handed to host memory for the entropy
-stage.  --steps 20 therefore times 320 4K frames.  All input frames are
+classify, transform, VAQ, quantize, reconstruct, in-loop deblock), the
+entropy precode, and each frame's block table + feed bits handed to host
+memory for the arithmetic coder.  --steps 20 therefore times 320 4K frames.  All input frames are
 resident in HBM before the timed region.
 
 Other legs (rank 0, N = 1), outside the timed region:
@@ -154,6 +154,16 @@ def record(cairo_amd, w, h, ring, q, t, payload, nbits):
     return buf[: (pos + 7) // 8].tobytes(), pos
 
 
+def payload(cairo_amd, ctx, out, ticket=None):
+    """A frame's payload (bytes, bits) from the context's outputs: the host
+    arithmetic coder over the GPU-precoded feed (or the host precode from the
+    planes when the feed overflowed)."""
+    if out.feed_status == cairo_amd.FEED_VALID:
+        return cairo_amd.serialize_feed(out.feed, out.feed_bits)
+    cy, cu, cv = (out.coef_y, out.coef_u, out.coef_v) if out.coef_y is not None else ctx.fetch_coef(ticket)
+    return cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ctx.ring, cy, cu, cv)
+
+
 def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None):
     """Submit frames [first, first+count) with up to `stages` in flight;
     on_frame(index, outputs) sees a frame's outputs before its release."""
@@ -163,7 +173,7 @@ def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None):
         f, t = inflight.popleft()
         out = ctx.wait(t, copy=False)
         if on_frame is not None:
-            on_frame(f, out)
+            on_frame(f, out, t)
         ctx.release(t)
 
     for f in range(first, first + count):
@@ -224,6 +234,7 @@ def main():
 
     ctx = share(cairo_amd.Context(w, h, ring, device=local))
     ctx.set_batch(batch)
+    ctx.set_outputs(cairo_amd.OUT_FEED)  # what the pipeline and the drop-in encoder hand to the host coder
     if a.rows:
         ctx.set_workgroups(a.rows)
     stages = ctx.stages
@@ -239,11 +250,9 @@ def main():
     n_check = min(n_check, warm_frames)
     hot_records = {}
 
-    def keep_record(f, out):
+    def keep_record(f, out, ticket):
         if f < n_check:
-            data, nbits = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, out.coef_y, out.coef_u,
-                                                    out.coef_v)
-            hot_records[f] = record(cairo_amd, w, h, ring, q, f, data, nbits)
+            hot_records[f] = record(cairo_amd, w, h, ring, q, f, *payload(cairo_amd, ctx, out, ticket))
 
     # warmup: frame 0 (I) + P-frames, in the same context and launches as the timed region
     run_hot_path(ctx, frame_ptr, 0, warm_frames, q, stages, keep_record)
@@ -379,6 +388,7 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
     try:
         ctx = share(cairo_amd.Context(w, h, ring, device=local))
         ctx.set_batch(batch)
+        ctx.set_outputs(cairo_amd.OUT_FEED)
         peers = [None] * world
         dist.all_gather_object(peers, ctx.peer_info(cross_device=True), group=gloo)
         ctx.join_group(rank, peers)
@@ -391,9 +401,7 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
                 n, t = inflight.popleft()
                 out = ctx.wait(t, copy=False)
                 if keep and n < n_check:
-                    data, nbits = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, out.coef_y, out.coef_u,
-                                                            out.coef_v)
-                    recs[n] = record(cairo_amd, w, h, ring, q, n, data, nbits)
+                    recs[n] = record(cairo_amd, w, h, ring, q, n, *payload(cairo_amd, ctx, out, t))
                 ctx.release(t)
 
             for n in range(first, first + count):
