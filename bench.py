@@ -79,6 +79,9 @@ def parse():
                    help="N > 1: skip the frame-interleaved single-stream leg")
     p.add_argument("--pmc", default=None, help="PMC summary json (profiles/) for roofline.traffic")
     p.add_argument("--batch", type=int, default=0, help="frames per engine launch (0 = library default)")
+    p.add_argument("--outputs", default="feed", choices=["feed", "coef"],
+                   help="what the timed context hands to the host: the GPU-precoded feed (the pipeline's mode) "
+                        "or the coefficient planes")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
     return p.parse_args()
 
@@ -234,7 +237,8 @@ def main():
 
     ctx = share(cairo_amd.Context(w, h, ring, device=local))
     ctx.set_batch(batch)
-    ctx.set_outputs(cairo_amd.OUT_FEED)  # what the pipeline and the drop-in encoder hand to the host coder
+    # what the pipeline and the drop-in encoder hand to the host coder
+    ctx.set_outputs(cairo_amd.OUT_FEED if a.outputs == "feed" else cairo_amd.OUT_COEF)
     if a.rows:
         ctx.set_workgroups(a.rows)
     stages = ctx.stages

@@ -441,7 +441,7 @@ def default_batch(width: int, height: int) -> int:
 def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):
     """Host entropy stage on explicit inputs -> (bytes, nbits)."""
     cap = capacity_bytes or (cy.size * 4 + 65536)
-    out = np.empty(cap, np.uint8)
+    out = np.zeros(cap, np.uint8)  # bits past the payload's end are left as they are: zeros
     pos = ctypes.c_uint32(0)
     t = np.ascontiguousarray(table).view(np.uint8)
     cy, cu, cv = (np.ascontiguousarray(a, dtype=np.int16) for a in (cy, cu, cv))
@@ -456,7 +456,7 @@ def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv
 def serialize_feed(feed: np.ndarray, feed_bits: int, capacity_bytes: int | None = None):
     """The arithmetic coder over a GPU-precoded feed (FrameOutputs.feed) -> (bytes, nbits)."""
     cap = capacity_bytes or (feed_bits // 8 * 2 + 65536)
-    out = np.empty(cap, np.uint8)
+    out = np.zeros(cap, np.uint8)
     pos = ctypes.c_uint32(0)
     f = np.ascontiguousarray(feed, dtype=np.uint32)
     _ck(lib().cairo_serialize_feed(_ptr(f), feed_bits, _ptr(out), cap, ctypes.byref(pos)), "cairo_serialize_feed")

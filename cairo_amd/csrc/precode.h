@@ -8,14 +8,18 @@ namespace cairo {
 
 // Header words of a frame's feed (device and mapped host copies): total
 // feed bits (lo, hi), overflow flag (a coefficient section exceeds the feed
-// stream's 32 Mbit: the host codes the frame itself), bits of the table lists.
-constexpr int kFeedHdrWords = 4;
+// stream's 32 Mbit: the host codes the frame itself), then the start bit of
+// each of the 11 lists (8 block-table lists, the Y, U and V sections).
+constexpr int kFeedHdrWords = 16;
+// Per-slot scratch words per macroblock: block lengths [6], table codes [8],
+// table positions [8], section offsets [3].
+constexpr int kFeedScratchPerMB = 25;
 
 // Feed capacity per staging slot, in 32-bit words: the table lists (at most
 // 103 bits per macroblock with 31-bit exp-Golomb codes) plus three
 // coefficient sections of at most 32 Mbit each, plus slack.
 inline size_t feed_words_per_slot(size_t mbs) {
-  return (103 * mbs + 3 * (size_t)kFeedCapacityBits) / 32 + 64;
+  return ((103 * mbs + 3 * (size_t)kFeedCapacityBits) / 32 + 64 + 15) & ~(size_t)15;  // 64-byte multiple
 }
 
 struct FeedArgs {
@@ -23,8 +27,8 @@ struct FeedArgs {
   const FrameArgs* fa;            // the launch's frame views (device)
   int slot[kMaxBatch];            // staging slot of frame j
   uint32_t* host[kMaxBatch];      // frame j's mapped pinned host buffer: header, then words
-  int32_t* lens;                  // per slot: 6 * mbs block lengths, then bit offsets
-  size_t lens_stride;
+  uint32_t* scratch;              // per slot: kFeedScratchPerMB * mbs words
+  size_t scratch_stride;
   uint32_t* feed;                 // per slot: feed words (device)
   size_t feed_stride;
   uint32_t* hdr;                  // per slot: kFeedHdrWords

@@ -11,14 +11,16 @@
 //   BR), then U, then V, each block ue(run) + se(zig-zag coefficients) with a
 //   delta DC.
 //
-// Three kernels per launch, on the launch's stream after the engine:
-//   k_feed_len    one wave per 8x8 coefficient block: its bits (zig-zag in
-//                 lanes, the run from a ballot, exp-Golomb lengths summed)
-//   k_feed_scan   one 1024-thread workgroup per frame: the block-table sections
-//                 (lengths, segmented "previous value" scans, codes), the
-//                 exclusive scan of the block lengths into bit offsets, the
-//                 section capacity check, zeroing of the feed words
-//   k_feed_write  one wave per block again: codes OR-ed in at their offsets
+// Four kernels per launch, on the launch's stream after the engine:
+//   k_feed_len    one wave per macroblock: the bits of its six 8x8 blocks
+//                 (zig-zag in lanes, the run from a ballot, exp-Golomb
+//                 lengths summed)
+//   k_feed_scan   one 1024-thread workgroup per frame over chunks of 1024
+//                 macroblocks: the table items' codes (segmented "previous
+//                 value" scans for the delta lists) and the exclusive scans of
+//                 the eleven lists' lengths, the section capacity check,
+//                 zeroing of the feed words
+//   k_feed_write  one wave per macroblock again: codes OR-ed in at their offsets
 //   k_feed_copy   the used words (and the header) to the frame's mapped
 //                 pinned host buffer
 // A coefficient section longer than the feed stream's 32 Mbit capacity
@@ -63,133 +65,76 @@ __device__ __forceinline__ void or_bits(uint32_t* w, uint64_t p, uint32_t code, 
   if (sh + len > 32) atomicOr(&w[(p >> 5) + 1], code >> (32 - sh));
 }
 
-// Coefficient block idx of a frame (feed order: Y blocks mb*4+sub, then U,
-// then V): plane pointer, pitch, origin, delta-DC reference (serialize.cpp:35-123).
-struct Blk {
-  const int16_t* p;
-  int pitch;
-  int16_t last_dc;
-  bool copy;
-};
-
-__device__ __forceinline__ Blk block_of(FA& a, int idx) {
-  const int mbs = a.wmb * a.hmb;
-  Blk b;
-  int mb, sub = 0, pl;
-  if (idx < 4 * mbs) {
-    mb = idx >> 2, sub = idx & 3, pl = 0;
-  } else {
-    mb = idx - 4 * mbs, pl = 1;
-    if (mb >= mbs) mb -= mbs, pl = 2;
-  }
+// The six 8x8 blocks of macroblock mb (Y TL, TR, BL, BR, U, V): this lane's
+// zig-zag coefficient of each (lane k = scan position k), with the delta DC
+// on lane 0 (serialize.cpp:35-123: the left neighbour's block at x - 8, or
+// the one above at y - 8 in the first column; stale output_cache values of
+// copy macroblocks included).  All six loads are issued together.
+__device__ __forceinline__ void mb_coefs(FA& a, int mb, int lane, int c[6]) {
   const int mx = mb % a.wmb, my = mb / a.wmb;
-  b.copy = (desc_at(a, mb).block_type & kCopy) != 0;
-  if (pl == 0) {
-    const int16_t* y = a.coef.y;
-    const int w = a.wa;
-    const int x0 = 16 * mx, y0 = 16 * my;
-    b.pitch = w;
-    b.p = y + (size_t)(y0 + 8 * (sub >> 1)) * w + x0 + 8 * (sub & 1);
-    if (sub == 0)
-      b.last_dc = mx > 0 ? y[(size_t)y0 * w + x0 - 8] : (my > 0 ? y[(size_t)(y0 - 8) * w + x0] : 0);
-    else if (sub == 3)
-      b.last_dc = y[(size_t)(y0 + 8) * w + x0];
-    else
-      b.last_dc = y[(size_t)y0 * w + x0];
-  } else {
-    const int16_t* c = pl == 1 ? a.coef.u : a.coef.v;
-    const int w = a.wa >> 1;
-    const int x0 = 8 * mx, y0 = 8 * my;
-    b.pitch = w;
-    b.p = c + (size_t)y0 * w + x0;
-    b.last_dc = mx > 0 ? c[(size_t)y0 * w + x0 - 8] : (my > 0 ? c[(size_t)(y0 - 8) * w + x0] : 0);
+  const int r = kZig[lane], ry = r >> 3, rx = r & 7;
+  const int16_t* y = a.coef.y;
+  const int16_t* u = a.coef.u;
+  const int16_t* v = a.coef.v;
+  const int w = a.wa, cw = a.wa >> 1;
+  const int x0 = 16 * mx, y0 = 16 * my, cx = 8 * mx, cy = 8 * my;
+#pragma unroll
+  for (int b = 0; b < 4; b++) c[b] = y[(size_t)(y0 + 8 * (b >> 1) + ry) * w + x0 + 8 * (b & 1) + rx];
+  c[4] = u[(size_t)(cy + ry) * cw + cx + rx];
+  c[5] = v[(size_t)(cy + ry) * cw + cx + rx];
+  if (lane == 0) {
+    const int16_t dy = mx > 0 ? y[(size_t)y0 * w + x0 - 8] : (my > 0 ? y[(size_t)(y0 - 8) * w + x0] : 0);
+    const int16_t du = mx > 0 ? u[(size_t)cy * cw + cx - 8] : (my > 0 ? u[(size_t)(cy - 8) * cw + cx] : 0);
+    const int16_t dv = mx > 0 ? v[(size_t)cy * cw + cx - 8] : (my > 0 ? v[(size_t)(cy - 8) * cw + cx] : 0);
+    const int16_t d0 = (int16_t)c[0], d2 = (int16_t)c[2];  // this MB's TL and BL DCs (lane 0 holds them)
+    c[0] = (int16_t)(c[0] - dy);
+    c[1] = (int16_t)(c[1] - d0);
+    c[2] = (int16_t)(c[2] - d0);
+    c[3] = (int16_t)(c[3] - d2);
+    c[4] = (int16_t)(c[4] - du);
+    c[5] = (int16_t)(c[5] - dv);
   }
-  return b;
 }
 
-// This lane's zig-zag coefficient (lane k of the wave = scan position k),
-// the block's run (last nonzero + 1) and this lane's code length.
-__device__ __forceinline__ int lane_coef(const Blk& b, int lane, int& run) {
-  const int r = kZig[lane];
-  int c = b.p[(size_t)(r >> 3) * b.pitch + (r & 7)];
-  if (lane == 0) c = (int16_t)(c - b.last_dc);
+__device__ __forceinline__ int run_of(int c) {
   const uint64_t nz = __ballot(c != 0);
-  run = nz ? 64 - __clzll(nz) : 0;
-  return c;
+  return nz ? 64 - __clzll(nz) : 0;
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Phase 1: one wave per macroblock, the bits of its six blocks.
 __global__ __launch_bounds__(256) void k_feed_len(FeedArgs f) {
   FA& a = ((FA*)f.fa)[blockIdx.y];
   const int mbs = a.wmb * a.hmb, lane = threadIdx.x & 63;
-  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (idx >= 6 * mbs) return;
-  const Blk b = block_of(a, idx);
-  int32_t* lens = f.lens + (size_t)f.slot[blockIdx.y] * f.lens_stride;
-  if (b.copy) {
-    if (lane == 0) lens[idx] = 0;
+  const int mb = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (mb >= mbs) return;
+  uint32_t* blen = f.scratch + (size_t)f.slot[blockIdx.y] * f.scratch_stride;  // [6][mbs]
+  if (a.table[mb].block_type & kCopy) {
+    if (lane < 6) blen[(size_t)lane * mbs + mb] = 0;
     return;
   }
-  int run;
-  const int c = lane_coef(b, lane, run);
-  uint32_t len = lane < run ? eg_len(se_val(c)) : 0u;
-  for (int o = 32; o; o >>= 1) len += __shfl_xor(len, o);
-  if (lane == 0) lens[idx] = (int32_t)(len + eg_len((uint32_t)run + 1u));
+  int c[6];
+  mb_coefs(a, mb, lane, c);
+  uint32_t mine = 0;
+#pragma unroll
+  for (int b = 0; b < 6; b++) {
+    const int run = run_of(c[b]);
+    const uint32_t t = wave_sum(lane < run ? eg_len(se_val(c[b])) : 0u) + eg_len((uint32_t)run + 1u);
+    if (lane == b) mine = t;
+  }
+  if (lane < 6) blen[(size_t)lane * mbs + mb] = mine;
 }
 
-constexpr int kScanT = 1024;
+// The table lists (serialize.cpp:156-286), then the three coefficient
+// sections, in feed order.
+enum { kTypes, kTargets, kMvx, kMvy, kSpPred, kSpAmount, kSpIndex, kQuality, kSecY, kSecU, kSecV, kLists };
+constexpr int kTabLists = kSecY;
 
-// Block-wide exclusive scan of one 64-bit value per thread; returns the
-// prefix, *total the sum.
-__device__ uint64_t block_scan(uint64_t v, uint64_t* sh, uint64_t* total) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint64_t x = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sh[w] = x;
-  __syncthreads();
-  if (t == 0) {
-    uint64_t s = 0;
-    for (int i = 0; i < kScanT / 64; i++) {
-      const uint64_t u = sh[i];
-      sh[i] = s;
-      s += u;
-    }
-    sh[kScanT / 64] = s;
-  }
-  __syncthreads();
-  const uint64_t r = sh[w] + x - v;
-  *total = sh[kScanT / 64];
-  __syncthreads();
-  return r;
-}
-
-// Segmented "latest present value" over threads: the value of the last
-// present item before this thread's run (0 if none) -- the reference's
-// `last` carried across the raster loop.
-__device__ int block_last(bool has, int last, int* sh_has, int* sh_val) {
-  const int t = threadIdx.x;
-  sh_has[t] = has ? t : -1;
-  sh_val[t] = last;
-  __syncthreads();
-  // inclusive max-scan of the index of the latest thread with an item
-  for (int o = 1; o < kScanT; o <<= 1) {
-    const int v = t >= o ? sh_has[t - o] : -1;
-    __syncthreads();
-    if (v > sh_has[t]) sh_has[t] = v;
-    __syncthreads();
-  }
-  const int src = t > 0 ? sh_has[t - 1] : -1;
-  const int r = src >= 0 ? sh_val[src] : 0;
-  __syncthreads();
-  return r;
-}
-
-// The table lists, in feed order.
-enum { kTypes, kTargets, kMvx, kMvy, kSpPred, kSpAmount, kSpIndex, kQuality, kLists };
-
-// Item of list L for MB d: present?, and (for the delta lists) its value.
+// Item of table list L for MB d: present?, and its value.
 __device__ __forceinline__ bool item(int L, const BlockDesc& d, int& value) {
   const bool intra = d.block_type & kIntra, motion = d.block_type & kMotion, copy = d.block_type & kCopy;
   switch (L) {
@@ -204,7 +149,7 @@ __device__ __forceinline__ bool item(int L, const BlockDesc& d, int& value) {
   }
 }
 
-// Code of an item given the previous present value of its list.
+// Code of an item given the previous present value of its list (delta lists).
 __device__ __forceinline__ uint32_t item_code(int L, int value, int prev, int tbits, uint32_t* len) {
   switch (L) {
     case kTypes: *len = 3; return (uint32_t)value;
@@ -220,127 +165,189 @@ __device__ __forceinline__ uint32_t item_code(int L, int value, int prev, int tb
   }
 }
 
+__device__ __forceinline__ bool delta_list(int L) { return L == kMvx || L == kMvy || L == kQuality; }
+
+constexpr int kScanT = 1024, kScanW = kScanT / 64;
+
+// Phase 2: one 1024-thread workgroup per frame walks the macroblocks in
+// chunks of 1024 (one per thread, coalesced): the table items' codes, the
+// delta lists' previous values (segmented scans), and the exclusive scans of
+// all eleven lists' lengths with carries across chunks.  Offsets are stored
+// relative to their list's start; the list bases follow from the totals.
 __global__ __launch_bounds__(kScanT) void k_feed_scan(FeedArgs f) {
-  __shared__ uint64_t sh[kScanT / 64 + 1];
-  __shared__ int sh_has[kScanT], sh_val[kScanT];
-  __shared__ uint64_t list_base[kLists + 1];
+  __shared__ uint32_t wsum[kScanW][kLists];
+  __shared__ int whas[kScanW][3], wval[kScanW][3];
+  __shared__ uint64_t carry_bits[kLists];
+  __shared__ int carry_has[3], carry_val[3];
   FA& a = ((FA*)f.fa)[blockIdx.x];
   const int slot = f.slot[blockIdx.x];
-  const int t = threadIdx.x, mbs = a.wmb * a.hmb;
-  const int per = (mbs + kScanT - 1) / kScanT, m0 = min(t * per, mbs), m1 = min(m0 + per, mbs);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, mbs = a.wmb * a.hmb;
   const int tbits = 31 - __clz(max(a.ring & 0xFF, 1));  // log2((uint8)R), serialize.cpp:179
-  uint32_t* feed = f.feed + (size_t)slot * f.feed_stride;
+  uint32_t* sc = f.scratch + (size_t)slot * f.scratch_stride;
+  const uint32_t* blen = sc;                  // [6][mbs]
+  uint32_t* tcode = sc + 6 * (size_t)mbs;     // [8][mbs]
+  uint32_t* tpos = tcode + 8 * (size_t)mbs;   // [8][mbs]: len << 26 | offset in list
+  uint32_t* boff = tpos + 8 * (size_t)mbs;    // [3][mbs]: offset of the MB's first block in its section
   uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
-  int32_t* lens = f.lens + (size_t)slot * f.lens_stride;
-
-  // ---- table lists: carry-in of the delta lists, lengths, offsets ----
-  int carry[kLists];
-  uint64_t off[kLists];
-  uint64_t base = 0;
-  for (int L = 0; L < kLists; L++) {
-    int last = 0;
-    bool has = false;
-    uint64_t bits = 0;
-    if (L == kMvx || L == kMvy || L == kQuality) {
-      for (int m = m0; m < m1; m++) {
-        int v;
-        if (item(L, desc_at(a, m), v)) has = true, last = v;
-      }
-      carry[L] = block_last(has, last, sh_has, sh_val);
+  if (t < kLists) carry_bits[t] = 0;
+  if (t < 3) carry_has[t] = 0, carry_val[t] = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < mbs; c0 += kScanT) {
+    const int mb = c0 + t;
+    const bool valid = mb < mbs;
+    BlockDesc d;
+    if (valid) {
+      d = a.table[mb];
     } else {
-      carry[L] = 0;
+      memset(&d, 0, sizeof(d));
+      d.block_type = kCopy;  // no items, no blocks
     }
-    int prev = carry[L];
-    for (int m = m0; m < m1; m++) {
-      int v;
-      if (!item(L, desc_at(a, m), v)) continue;
-      uint32_t len;
-      item_code(L, v, prev, tbits, &len);
-      bits += len;
-      prev = v;
+    // the delta lists' previous values: segmented "last present" scans
+    int val[kTabLists], prev[3];
+    bool has[kTabLists];
+#pragma unroll
+    for (int L = 0; L < kTabLists; L++) has[L] = valid && item(L, d, val[L]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int L = k == 0 ? kMvx : (k == 1 ? kMvy : kQuality);
+      int hv = has[L], vv = val[L];  // inclusive within the wave
+      for (int o = 1; o < 64; o <<= 1) {
+        const int h2 = __shfl_up(hv, o), v2 = __shfl_up(vv, o);
+        if (lane >= o && !hv) hv = h2, vv = v2;
+      }
+      if (lane == 63) whas[w][k] = hv, wval[w][k] = vv;
+      const int he = __shfl_up(hv, 1), ve = __shfl_up(vv, 1);  // exclusive within the wave
+      prev[k] = lane > 0 && he ? ve : 0x7FFFFFFF;                // 0x7FFFFFFF: look further back
     }
-    uint64_t total;
-    off[L] = base + block_scan(bits, sh, &total);
-    if (t == 0) list_base[L] = base;
-    base += total;
+    // the lengths
+    uint32_t len[kLists], code[kTabLists];
+#pragma unroll
+    for (int L = 0; L < kTabLists; L++) len[L] = 0, code[L] = 0;
+    len[kSecY] = valid ? blen[mb] + blen[mbs + mb] + blen[2 * (size_t)mbs + mb] + blen[3 * (size_t)mbs + mb] : 0;
+    len[kSecU] = valid ? blen[4 * (size_t)mbs + mb] : 0;
+    len[kSecV] = valid ? blen[5 * (size_t)mbs + mb] : 0;
+    __syncthreads();  // whas / wval complete
+    if (t < 3) {  // waves' carries, in order: the last present value before each wave
+      int hv = carry_has[t], vv = carry_val[t];
+      for (int i = 0; i < kScanW; i++) {
+        const int h2 = whas[i][t], v2 = wval[i][t];
+        whas[i][t] = hv, wval[i][t] = vv;
+        if (h2) hv = 1, vv = v2;
+      }
+      carry_has[t] = hv, carry_val[t] = vv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int L = k == 0 ? kMvx : (k == 1 ? kMvy : kQuality);
+      if (prev[k] == 0x7FFFFFFF) prev[k] = whas[w][k] ? wval[w][k] : 0;
+      if (has[L]) code[L] = item_code(L, val[L], prev[k], tbits, &len[L]);
+    }
+#pragma unroll
+    for (int L = 0; L < kTabLists; L++)
+      if (has[L] && !delta_list(L)) code[L] = item_code(L, val[L], 0, tbits, &len[L]);
+    // exclusive scans of the eleven lengths
+    uint32_t inc[kLists];
+#pragma unroll
+    for (int L = 0; L < kLists; L++) {
+      uint32_t x = len[L];
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      inc[L] = x;
+      if (lane == 63) wsum[w][L] = x;
+    }
+    __syncthreads();
+    if (t < kLists) {  // wave prefixes, plus the running carry of the list
+      uint64_t s = carry_bits[t];
+      for (int i = 0; i < kScanW; i++) {
+        const uint32_t u = wsum[i][t];
+        wsum[i][t] = (uint32_t)s;  // offsets within a list stay below 2^26 (else overflow, below)
+        s += u;
+      }
+      carry_bits[t] = s;
+    }
+    __syncthreads();
+    if (valid) {
+#pragma unroll
+      for (int L = 0; L < kTabLists; L++) {
+        const uint32_t off = wsum[w][L] + inc[L] - len[L];
+        tcode[(size_t)L * mbs + mb] = code[L];
+        tpos[(size_t)L * mbs + mb] = has[L] ? (len[L] << 26) | (off & 0x3FFFFFFu) : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) boff[(size_t)k * mbs + mb] = wsum[w][kSecY + k] + inc[kSecY + k] - len[kSecY + k];
+    }
+    __syncthreads();  // wsum / whas reused by the next chunk
   }
-  const uint64_t table_bits = base;
-
-  // ---- coefficient blocks: exclusive scan of the lengths, sections Y, U, V ----
-  const int nb = 6 * mbs, bper = (nb + kScanT - 1) / kScanT;
-  const int b0 = min(t * bper, nb), b1 = min(b0 + bper, nb);
-  uint64_t s = 0;
-  for (int i = b0; i < b1; i++) s += (uint32_t)lens[i];
-  uint64_t total;
-  uint64_t o = table_bits + block_scan(s, sh, &total);
-  for (int i = b0; i < b1; i++) {  // lengths -> offsets, in place (as int32 offsets from table_bits)
-    const uint32_t l = (uint32_t)lens[i];
-    lens[i] = (int32_t)(o - table_bits);
-    o += l;
+  // list bases, capacity, header; then zero the words the writer ORs into
+  __shared__ uint64_t all_bits;
+  __shared__ int over;
+  if (t == 0) {
+    uint64_t b = 0;
+    for (int L = 0; L < kLists; L++) {
+      hdr[4 + L] = (uint32_t)b;
+      b += carry_bits[L];
+    }
+    const bool o = carry_bits[kSecY] > kFeedCapacityBits || carry_bits[kSecU] > kFeedCapacityBits ||
+                   carry_bits[kSecV] > kFeedCapacityBits || b + 64 > (uint64_t)f.feed_stride * 32;
+    hdr[0] = (uint32_t)b;
+    hdr[1] = (uint32_t)(b >> 32);
+    hdr[2] = o ? 1u : 0u;
+    all_bits = b;
+    over = o;
   }
   __syncthreads();
-  const uint64_t all = table_bits + total;
-  // section sizes: Y = blocks [0, 4 mbs), U = [4 mbs, 5 mbs), V = the rest
-  __shared__ uint64_t sec[3];
-  if (t == 0) {
-    const uint64_t u0 = (uint64_t)(uint32_t)lens[4 * mbs], v0 = (uint64_t)(uint32_t)lens[5 * mbs];
-    sec[0] = u0, sec[1] = v0 - u0, sec[2] = total - v0;
-  }
-  __syncthreads();
-  const bool overflow = sec[0] > kFeedCapacityBits || sec[1] > kFeedCapacityBits || sec[2] > kFeedCapacityBits ||
-                        all + 64 > (uint64_t)f.feed_stride * 32;
-  if (t == 0) {
-    hdr[0] = (uint32_t)all;
-    hdr[1] = (uint32_t)(all >> 32);
-    hdr[2] = overflow ? 1u : 0u;
-    hdr[3] = (uint32_t)table_bits;
-  }
-  if (overflow) return;  // the host codes this frame itself (k_feed_write / k_feed_copy see the flag)
-  // ---- zero the words, then write the table lists ----
-  const uint64_t words = (all + 31) / 32 + 1;
+  if (over) return;  // the host codes this frame from its planes
+  uint32_t* feed = f.feed + (size_t)slot * f.feed_stride;
+  const uint64_t words = (all_bits + 31) / 32 + 1;
   for (uint64_t i = t; i < words; i += kScanT) feed[i] = 0;
-  __syncthreads();
-  for (int L = 0; L < kLists; L++) {
-    int prev = carry[L];
-    uint64_t p = off[L];
-    for (int m = m0; m < m1; m++) {
-      int v;
-      if (!item(L, desc_at(a, m), v)) continue;
-      uint32_t len;
-      const uint32_t code = item_code(L, v, prev, tbits, &len);
-      or_bits(feed, p, code, len);
-      p += len;
-      prev = v;
-    }
-  }
 }
 
+// Phase 3: one wave per macroblock: its table items (lanes 0..7) and its
+// six blocks' codes, OR-ed in at their offsets.
 __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
   FA& a = ((FA*)f.fa)[blockIdx.y];
   const int slot = f.slot[blockIdx.y];
-  if (f.hdr[(size_t)slot * kFeedHdrWords + 2]) return;  // overflow: the host codes this frame
+  const uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
+  if (hdr[2]) return;  // overflow: the host codes this frame
   const int mbs = a.wmb * a.hmb, lane = threadIdx.x & 63;
-  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (idx >= 6 * mbs) return;
-  const Blk b = block_of(a, idx);
-  if (b.copy) return;
-  int run;
-  const int c = lane_coef(b, lane, run);
-  const uint32_t val = se_val(c);
-  const uint32_t len = lane < run ? eg_len(val) : 0u;
-  uint32_t x = len;  // inclusive prefix of the lane lengths
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  const uint64_t base = (uint64_t)f.hdr[(size_t)slot * kFeedHdrWords + 3] +
-                        (uint32_t)f.lens[(size_t)slot * f.lens_stride + idx];
+  const int mb = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (mb >= mbs) return;
+  const uint32_t* sc = f.scratch + (size_t)slot * f.scratch_stride;
+  const uint32_t* tcode = sc + 6 * (size_t)mbs;
+  const uint32_t* tpos = tcode + 8 * (size_t)mbs;
+  const uint32_t* boff = tpos + 8 * (size_t)mbs;
   uint32_t* feed = f.feed + (size_t)slot * f.feed_stride;
-  const uint32_t ul = eg_len((uint32_t)run + 1u);
-  if (lane == 0) or_bits(feed, base, eg_code((uint32_t)run + 1u), ul);
-  if (lane < run) or_bits(feed, base + ul + (x - len), eg_code(val), len);
+  if (lane < kTabLists) {
+    const uint32_t p = tpos[(size_t)lane * mbs + mb];
+    or_bits(feed, (uint64_t)hdr[4 + lane] + (p & 0x3FFFFFFu), tcode[(size_t)lane * mbs + mb], p >> 26);
+  }
+  if (a.table[mb].block_type & kCopy) return;
+  int c[6];
+  mb_coefs(a, mb, lane, c);
+  uint64_t pos = (uint64_t)hdr[4 + kSecY] + boff[mb];
+#pragma unroll
+  for (int b = 0; b < 6; b++) {
+    if (b == 4) pos = (uint64_t)hdr[4 + kSecU] + boff[(size_t)mbs + mb];
+    if (b == 5) pos = (uint64_t)hdr[4 + kSecV] + boff[2 * (size_t)mbs + mb];
+    const int run = run_of(c[b]);
+    const uint32_t val = se_val(c[b]);
+    const uint32_t len = lane < run ? eg_len(val) : 0u;
+    uint32_t x = len;  // inclusive prefix of the lane lengths
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    const uint32_t ul = eg_len((uint32_t)run + 1u);
+    if (lane == 0) or_bits(feed, pos, eg_code((uint32_t)run + 1u), ul);
+    if (lane < run) or_bits(feed, pos + ul + (x - len), eg_code(val), len);
+    pos += ul + __shfl(x, 63);
+  }
 }
 
+// Phase 4: the used words and the header into the frame's mapped pinned buffer.
 __global__ __launch_bounds__(256) void k_feed_copy(FeedArgs f) {
   const int j = blockIdx.y, slot = f.slot[j];
   const uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
@@ -356,7 +363,7 @@ __global__ __launch_bounds__(256) void k_feed_copy(FeedArgs f) {
 }  // namespace
 
 hipError_t launch_precode(const FeedArgs& f, int mbs, hipStream_t s) {
-  const dim3 blocks((6 * mbs + 3) / 4, f.nframes);
+  const dim3 blocks((mbs + 3) / 4, f.nframes);
   hipLaunchKernelGGL(k_feed_len, blocks, dim3(256), 0, s, f);
   hipLaunchKernelGGL(k_feed_scan, dim3(f.nframes), dim3(kScanT), 0, s, f);
   hipLaunchKernelGGL(k_feed_write, blocks, dim3(256), 0, s, f);
