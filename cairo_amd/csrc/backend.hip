@@ -21,6 +21,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -137,6 +138,7 @@ struct cairo_ctx {
   // next launch back (A/B at 4K: 3583 vs 3768 Mpix/s).
   hipStream_t ps = nullptr;
   hipEvent_t pre_done[kSyncAreas] = {};
+  bool ps_own = getenv("CAIRO_PRECODE_OWN_STREAM") != nullptr;  // A/B switch
   bool sys = false;           // a member is another process or device: system-scope hand-offs
   int32_t *sync = nullptr, *sticky = nullptr;
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
@@ -411,9 +413,10 @@ int flush(cairo_ctx* c) {
   }
   const int last = c->pend[e.nframes - 1].slot;
   if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
-  CK(hipEventRecord(c->batch_end[area], st));
+  hipStream_t pst = c->ps_own ? c->ps : st;
+  if (c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
   if (c->outputs & CAIRO_OUT_FEED) {  // the entropy precode, straight into mapped host memory
-    CK(hipStreamWaitEvent(c->ps, c->batch_end[area], 0));
+    if (c->ps_own) CK(hipStreamWaitEvent(c->ps, c->batch_end[area], 0));
     FeedArgs fa;
     memset(&fa, 0, sizeof(fa));
     fa.nframes = e.nframes;
@@ -427,7 +430,10 @@ int flush(cairo_ctx* c) {
     fa.feed = c->feed_dev;
     fa.feed_stride = c->feed_words;
     fa.hdr = c->feed_hdr;
-    CK(launch_precode(fa, (int)c->mbs, c->ps));
+    CK(launch_precode(fa, (int)c->mbs, pst));
+  }
+  if (!c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
+  if (c->ps_own && (c->outputs & CAIRO_OUT_FEED)) {
     CK(hipEventRecord(c->pre_done[area], c->ps));
     CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
   } else {

@@ -15,7 +15,7 @@
 //   k_feed_len    one wave per macroblock: the bits of its six 8x8 blocks
 //                 (zig-zag in lanes, the run from a ballot, exp-Golomb
 //                 lengths summed)
-//   k_feed_scan   one 1024-thread workgroup per frame over chunks of 1024
+//   k_feed_scan   one 256-thread workgroup per frame over chunks of 256
 //                 macroblocks: the table items' codes (segmented "previous
 //                 value" scans for the delta lists) and the exclusive scans of
 //                 the eleven lists' lengths, the section capacity check,
@@ -167,10 +167,12 @@ __device__ __forceinline__ uint32_t item_code(int L, int value, int prev, int tb
 
 __device__ __forceinline__ bool delta_list(int L) { return L == kMvx || L == kMvy || L == kQuality; }
 
-constexpr int kScanT = 1024, kScanW = kScanT / 64;
+constexpr int kScanT = 256, kScanW = kScanT / 64;  // small workgroups fit beside the persistent engine
 
-// Phase 2: one 1024-thread workgroup per frame walks the macroblocks in
-// chunks of 1024 (one per thread, coalesced): the table items' codes, the
+// Phase 2: one 256-thread workgroup per frame walks the macroblocks in
+// chunks of 256 (one per thread, coalesced; a workgroup that small fits
+// beside the persistent engine's, so it runs in the slots a finishing launch
+// frees): the table items' codes, the
 // delta lists' previous values (segmented scans), and the exclusive scans of
 // all eleven lists' lengths with carries across chunks.  Offsets are stored
 // relative to their list's start; the list bases follow from the totals.
@@ -305,6 +307,10 @@ __global__ __launch_bounds__(kScanT) void k_feed_scan(FeedArgs f) {
   for (uint64_t i = t; i < words; i += kScanT) feed[i] = 0;
 }
 
+// Words an 8x8 block's codes can span: ue(65) (13 bits) + 64 codes of at
+// most 31 bits, from any bit of a word.
+constexpr int kBlockWords = (13 + 64 * 31 + 31) / 32 + 1;
+
 // Phase 3: one wave per macroblock: its table items (lanes 0..7) and its
 // six blocks' codes, OR-ed in at their offsets.
 __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
@@ -325,6 +331,11 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
     or_bits(feed, (uint64_t)hdr[4 + lane] + (p & 0x3FFFFFFu), tcode[(size_t)lane * mbs + mb], p >> 26);
   }
   if (a.table[mb].block_type & kCopy) return;
+  // A block's codes are assembled in LDS words, then stored: the words inside
+  // its bit range belong to it alone (plain stores); only its first and last
+  // word are shared with the neighbouring blocks (global atomic OR).
+  __shared__ uint32_t stage[4][kBlockWords];
+  uint32_t* sw = stage[threadIdx.x >> 6];
   int c[6];
   mb_coefs(a, mb, lane, c);
   uint64_t pos = (uint64_t)hdr[4 + kSecY] + boff[mb];
@@ -341,9 +352,24 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
       if (lane >= o) x += y;
     }
     const uint32_t ul = eg_len((uint32_t)run + 1u);
-    if (lane == 0) or_bits(feed, pos, eg_code((uint32_t)run + 1u), ul);
-    if (lane < run) or_bits(feed, pos + ul + (x - len), eg_code(val), len);
-    pos += ul + __shfl(x, 63);
+    const uint64_t end = pos + ul + __shfl(x, 63);
+    const uint64_t w0 = pos >> 5;
+    const int nw = (int)(((end + 31) >> 5) - w0);  // <= kBlockWords
+    for (int i = lane; i < nw; i += 64) sw[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t rel = (uint32_t)(pos & 31);
+    if (lane == 0) or_bits(sw, rel, eg_code((uint32_t)run + 1u), ul);
+    if (lane < run) or_bits(sw, rel + ul + (x - len), eg_code(val), len);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < nw; i += 64) {
+      if (i == 0 || i == nw - 1)
+        atomicOr(&feed[w0 + i], sw[i]);
+      else
+        feed[w0 + i] = sw[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    pos = end;
   }
 }
 
