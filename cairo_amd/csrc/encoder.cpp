@@ -6,6 +6,7 @@
 // quantize, reconstruct, deblock, and the entropy precode), the arithmetic
 // coder on the host appended to the caller's bit_stream, then the
 // reference's frame-state update.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -81,6 +82,7 @@ class gpu_encoder : public evx1_encoder {
     frame_t f = frame_;
     if (evx_failed(output->write_bytes(&f, sizeof(f)))) return EVX_ERROR_EXECUTION_FAILURE;
 
+    const auto t0 = std::chrono::steady_clock::now();
     int ticket = -1;
     int r = cairo_ctx_submit(ctx_, (const uint8_t *)image, 0, frame_.index, frame_.type,
                              frame_.quality, &ticket);
@@ -91,8 +93,16 @@ class gpu_encoder : public evx1_encoder {
       cairo_ctx_release(ctx_, ticket);
       return EVX_ERROR_EXECUTION_FAILURE;
     }
+    const auto t1 = std::chrono::steady_clock::now();
     uint64_t pos = output->query_write_index();
     r = cairo::serialize_result(ctx_, ticket, &res, ring_, output->query_data(), output->query_capacity(), &pos);
+    if (trace_) {  // CAIRO_ENCODE_TRACE=1: where a synchronous encode() spends its time
+      const auto t2 = std::chrono::steady_clock::now();
+      fprintf(stderr, "[cairo_amd] encode frame %u: gpu+transfers %.3f ms, host coder %.3f ms (feed %s)\n",
+              frame_.index, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(),
+              res.feed_status == CAIRO_FEED_VALID ? "gpu" : "host");
+    }
     memcpy(last_table_, res.block_table, (size_t)res.wmb * res.hmb * 16);
     cairo_ctx_release(ctx_, ticket);
     if (r) return EVX_ERROR_EXECUTION_FAILURE;
@@ -204,6 +214,7 @@ class gpu_encoder : public evx1_encoder {
   }
 
   bool initialized_ = false;
+  const bool trace_ = getenv("CAIRO_ENCODE_TRACE") != nullptr;
   frame_t frame_;
   uint32 width_ = 0, height_ = 0;
   uint32 ring_ = kDefaultRing;
