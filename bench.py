@@ -82,6 +82,7 @@ def parse():
     p.add_argument("--outputs", default="feed", choices=["feed", "coef"],
                    help="what the timed context hands to the host: the GPU-precoded feed (the pipeline's mode) "
                         "or the coefficient planes")
+    p.add_argument("--helpers", type=int, default=0, help="helper workgroups of a launch's workers (0 = default)")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
     return p.parse_args()
 
@@ -241,6 +242,8 @@ def main():
     ctx.set_outputs(cairo_amd.OUT_FEED if a.outputs == "feed" else cairo_amd.OUT_COEF)
     if a.rows:
         ctx.set_workgroups(a.rows)
+    if a.helpers:
+        ctx.set_helpers(a.helpers)
     stages = ctx.stages
 
     def barrier():

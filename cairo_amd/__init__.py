@@ -89,6 +89,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_peer_info": (I, [P, I, P]),
         "cairo_ctx_join_group": (I, [P, I, I, P]),
         "cairo_ctx_flush": (I, [P]),
+        "cairo_ctx_set_helpers": (I, [P, I]),
         "cairo_ctx_max_workgroups": (I, [P]),
         "cairo_default_batch": (I, [U, U]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
@@ -354,6 +355,9 @@ class Context:
 
     def set_workgroups(self, rows: int = 0) -> None:
         _ck(self.L.cairo_ctx_set_workgroups(self.h, rows), "set_workgroups")
+
+    def set_helpers(self, helpers: int = 0) -> None:
+        _ck(self.L.cairo_ctx_set_helpers(self.h, helpers), "set_helpers")
 
     def max_workgroups(self) -> int:
         return int(self.L.cairo_ctx_max_workgroups(self.h))

@@ -157,6 +157,7 @@ struct cairo_ctx {
   int npend = 0;
   int last_slot = -1;  // slot of the last launched frame
   int wg_rows = 0;
+  int wg_helpers = 0;  // helpers of the launch's 2 * wg_rows workgroups (0: half)
   int max_rows = 0;  // row coders (= helpers) per launch that stay co-resident with the other in-flight launch
   bool profiling = false;
   TimedBatch tb[kLaunchSlots];
@@ -370,9 +371,13 @@ int flush(cairo_ctx* c) {
   const int area = (int)(b % kSyncAreas);
   e.sync = c->sync + (size_t)area * c->sync_words;
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
-  e.n_rows = c->wg_rows > 0 ? std::min(c->wg_rows, c->max_rows) : c->max_rows;
-  if (e.n_rows > rows) e.n_rows = rows;
-  e.n_helpers = e.n_rows;
+  {  // half of the resident slots per launch, split between the pools
+    const int total = 2 * (c->wg_rows > 0 ? std::min(c->wg_rows, c->max_rows) : c->max_rows);
+    int nh = c->wg_helpers > 0 ? std::min(c->wg_helpers, total - 1) : total / 2;
+    int nr = total - nh;
+    e.n_helpers = std::max(1, std::min(nh, rows));
+    e.n_rows = std::max(1, std::min(nr, rows));
+  }
   // this sync area was last used by launch b-3 (only a launch reads its own
   // area); launch b-2 precedes this one on the same stream
   if (b >= 3) CK(hipStreamWaitEvent(st, c->batch_end[(b - 3) % kSyncAreas], 0));
@@ -659,6 +664,13 @@ int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
   if (!c || rows < 0 || rows > c->max_rows) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   c->wg_rows = rows;
+  return kSuccess;
+}
+
+int cairo_ctx_set_helpers(cairo_ctx* c, int helpers) {
+  if (!c || helpers < 0 || helpers >= 2 * c->max_rows) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->wg_helpers = helpers;
   return kSuccess;
 }
 

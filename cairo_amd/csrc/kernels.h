@@ -158,7 +158,7 @@ struct EngineArgs {
   int32_t* sync;           // SyncLayout words of this launch
   int32_t* sticky;
   uint64_t* stamps;
-  int n_helpers, n_rows;   // worker pools (workgroups, equal sizes), interleaved in blockIdx runs of 8
+  int n_helpers, n_rows;   // worker pools (workgroups), spread over the block indices (is_helper)
   int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)
   const int32_t* order;    // [nframes * hmb] task order of every pool: (frame << 16 | row),
                            // sorted by (row + kOrderSlope * frame, frame)

@@ -1884,7 +1884,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 // ---------------------------------------------------------------------------
 // The engine: one persistent launch encodes a batch of consecutive frames,
 // pipelined across frames.  Two worker pools (helpers and row coders,
-// interleaved in blockIdx runs of 8: is_helper) dequeue (frame, row) tasks in e.order (by row + slope * frame):
+// spread over the block indices: is_helper) dequeue (frame, row) tasks in e.order (by row + slope * frame):
 //   helper (j, r): inter search of row r, group g (MBs 4g..4g+3) once the
 //           previous frame is final on MB rows r-2..r+2 over the group's
 //           search window [64g-32, 64g+96) (this also covers every older
@@ -1903,13 +1903,12 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 
 constexpr int kPrioFrameMBs = 4000;  // helpers get issue priority above this frame size
 
-// Pool of workgroup b out of n (n/2 helpers, n/2 row coders): blocks
-// alternate in runs of 8, one run per XCD in dispatch order, so both pools
-// are spread over every XCD and a launch that is only partly resident (a
-// shared or partitioned GPU) still has workers of both pools.
-__device__ __forceinline__ bool is_helper(int b, int n) {
-  const int full = n & ~15;
-  return b < full ? (b & 15) < 8 : (b - full) < ((n - full) >> 1);
+// Pool of workgroup b out of n, nh of them helpers: spread evenly over the
+// block indices (so over every XCD, which take blocks round-robin), and a
+// launch that is only partly resident (a shared or partitioned GPU) still
+// has workers of both pools.
+__device__ __forceinline__ bool is_helper(int b, int nh, int n) {
+  return ((b + 1) * nh) / n > (b * nh) / n;
 }
 
 template <bool kDecode>
@@ -1921,7 +1920,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   if (ks && threadIdx.x == 0)
     __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int total = e.nframes * hmb;
-  if (is_helper(b, e.n_helpers + e.n_rows)) {
+  if (is_helper(b, e.n_helpers, e.n_helpers + e.n_rows)) {
     // The helpers' inter records gate every row coder at its group starts:
     // on large frames they win the SIMD issue arbitration against the coders'
     // waves (A/B: 1080p +3 %, 4K +3 %; 720p -1 %, so not there).

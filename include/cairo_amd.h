@@ -178,6 +178,9 @@ CAIRO_API int cairo_ctx_set_outputs(cairo_ctx *ctx, int outputs);
 /* The coefficient planes of a waited, unreleased frame (a D2H copy from its
  * staging slot when the context does not copy them already). */
 CAIRO_API int cairo_ctx_fetch_coef(cairo_ctx *ctx, int ticket, cairo_frame_result *out);
+/* Of a launch's 2 * workgroups workers, how many are row helpers (inter
+ * search + deblock) rather than row coders (0: half). */
+CAIRO_API int cairo_ctx_set_helpers(cairo_ctx *ctx, int helpers);
 /* Upper bound of cairo_ctx_set_workgroups on this device. */
 CAIRO_API int cairo_ctx_max_workgroups(const cairo_ctx *ctx);
 

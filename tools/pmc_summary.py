@@ -151,6 +151,38 @@ def main():
                                         "engine_busy_ms_per_frame": b["roofline"]["engine_busy_ms_per_frame"],
                                         "avg_launch_ms": b["roofline"]["avg_launch_ms"],
                                         "frac": b["roofline"]["frac"]}
+    # read requests by size (TCC_EA0_RDREQ_32B / 64B / 128B) and the uncached
+    # 32-byte ones (agent-scope hand-off polls and granule loads): bytes by
+    # request size, no blanket FETCH_SIZE correction
+    rs = os.path.join(a.src, "prof_rdsize", "run_counter_collection.csv")
+    rq = os.path.join(a.src, "prof_req", "run_counter_collection.csv")
+    if os.path.exists(rs):
+        med = {}
+        for cn in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum",
+                   "TCC_EA0_RD_UNCACHED_32B_sum"):
+            v = per_kernel(rs, cn).get("engine")
+            if v:
+                med[cn] = statistics.median(v)
+        if os.path.exists(rq):
+            for cn in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"):
+                v = per_kernel(rq, cn).get("engine")
+                if v:
+                    med[cn] = statistics.median(v)
+        if med:
+            n32, n64, n128 = (med.get(f"TCC_EA0_RDREQ_{k}_sum", 0) for k in ("32B", "64B", "128B"))
+            rd = 32 * n32 + 64 * n64 + 128 * n128
+            wr = (64 * med["TCC_EA0_WRREQ_64B_sum"] + 32 * (med["TCC_EA0_WRREQ_sum"] - med["TCC_EA0_WRREQ_64B_sum"])
+                  if "TCC_EA0_WRREQ_sum" in med else None)
+            res["engine_requests_per_launch"] = med
+            res["engine_read_bytes_by_size_per_frame"] = int(rd / a.batch)
+            res["engine_read_uncached_32b_share"] = round(med.get("TCC_EA0_RD_UNCACHED_32B_sum", 0) /
+                                                          max(n32 + n64 + n128, 1), 4)
+            if wr is not None:
+                res["engine_write_bytes_by_size_per_frame"] = int(wr / a.batch)
+                res["per_frame_hbm_bytes_sized"] = int((rd + wr) / a.batch)
+            if "TCC_EA0_RDREQ_DRAM_sum" in med and "TCC_EA0_RDREQ_sum" in med:
+                res["engine_read_requests_dram_share"] = round(med["TCC_EA0_RDREQ_DRAM_sum"] /
+                                                               max(med["TCC_EA0_RDREQ_sum"], 1), 4)
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws
