@@ -296,8 +296,8 @@ def main():
     pmc_path = a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-        k = pmc.get("per_frame_hbm_bytes", {}).get("engine")
-        if k is not None:
+        k = pmc.get("per_frame_hbm_bytes_sized") or pmc.get("per_frame_hbm_bytes", {}).get("engine")
+        if k is not None:  # by request size (TCC_EA0_RDREQ_32B/64B/128B, WRREQ) when profiled so
             roof["traffic"] = k
             roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         ws = pmc.get("engine_wave_states")

@@ -900,9 +900,10 @@ int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
     CK(hipMalloc(&c->feed_hdr, kFeedHdrWords * 4 * S));
     CK(hipMalloc(&c->feed_scratch, kFeedScratchPerMB * c->mbs * 4 * S));
     CK(hipHostMalloc(&c->feed_host, (kFeedHdrWords + c->feed_words) * 4 * S, hipHostMallocMapped));
-    CK(hipStreamCreateWithFlags(&c->fs, hipStreamNonBlocking));
-    CK(hipStreamCreateWithFlags(&c->ps, hipStreamNonBlocking));
-    for (auto& ev : c->pre_done) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (c->ps_own) {  // (the A/B variant: each stream takes a hardware queue)
+      CK(hipStreamCreateWithFlags(&c->ps, hipStreamNonBlocking));
+      for (auto& ev : c->pre_done) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
   }
   c->outputs = outputs;
   return kSuccess;
@@ -919,10 +920,13 @@ int cairo_ctx_fetch_coef(cairo_ctx* c, int ticket, cairo_frame_result* out) {
   CK(hipEventSynchronize(s.d2h_done));  // the frame's engine launch has finished
   const int slot = ticket % c->stages;
   if (!(c->outputs & CAIRO_OUT_COEF)) {  // still in the staging slot until its release
-    hipStream_t fs = c->fs ? c->fs : c->cs;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (!c->fs) CK(hipStreamCreateWithFlags(&c->fs, hipStreamNonBlocking));  // rare: made on first use
+    }
     CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2, hipMemcpyDeviceToHost,
-                      fs));
-    CK(hipStreamSynchronize(fs));
+                      c->fs));
+    CK(hipStreamSynchronize(c->fs));
   }
   out->coef_y = s.coef;
   out->coef_u = s.coef + (size_t)c->wa * c->ha;

@@ -350,26 +350,47 @@ __device__ __forceinline__ uint4 bias4(uint4 v) {
 // columns multiples of 16; chroma rows [r0/2, r1/2), columns halved) with
 // origin (ox, oy) (luma pixels, multiples of 16) from plane set p, biased.
 // All 256 threads participate.
+#ifndef CAIRO_WIN_UNROLL
+#define CAIRO_WIN_UNROLL 4
+#endif
+constexpr int kWinUnroll = CAIRO_WIN_UNROLL;
+
 __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa, int ha, int ox,
                                             int oy, int r0, int r1, int c0, int c1) {
+  // All of a thread's 16-byte loads are issued before the first LDS store
+  // (kWinUnroll in flight): the staging costs one fabric round trip instead
+  // of one per chunk.
   const int nc = (c1 - c0) >> 3, nl = (r1 - r0) * nc;  // 16-B chunks per row / in all
-  for (int k = threadIdx.x; k < nl; k += 256) {
-    const int r = r0 + k / nc, c = c0 + (k % nc) * 8;
-    const int gy = oy + r, gx = ox + c;
-    if (gy >= 0 && gy < ha && gx >= 0 && gx < wa)
-      *(uint4*)&w.y[r * kWinLP + c] = bias4(*(const uint4*)&p.y[(size_t)gy * wa + gx]);
-  }
   const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
   const int ncc = nc >> 1, ncl = ((r1 >> 1) - (r0 >> 1)) * ncc;  // chroma rows [r0/2, r1/2)
-  for (int k = threadIdx.x; k < 2 * ncl; k += 256) {
-    const int pl = k >= ncl, kk = k - pl * ncl;
-    const int r = (r0 >> 1) + kk / ncc, c = (c0 >> 1) + (kk % ncc) * 8;
-    const int gy = coy + r, gx = cox + c;
-    if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
-      const int16_t* src = pick(p, 1 + pl);
-      int16_t* dst = pl ? w.v : w.u;
-      *(uint4*)&dst[r * kWinCP + c] = bias4(*(const uint4*)&src[(size_t)gy * cw + gx]);
+  const int n = nl + 2 * ncl;
+  for (int k0 = threadIdx.x; k0 < n; k0 += 256 * kWinUnroll) {
+    uint4 v[kWinUnroll];
+    int16_t* dst[kWinUnroll];
+#pragma unroll
+    for (int u = 0; u < kWinUnroll; u++) {
+      const int k = k0 + 256 * u;
+      dst[u] = nullptr;
+      if (k < nl) {
+        const int r = r0 + k / nc, c = c0 + (k % nc) * 8;
+        const int gy = oy + r, gx = ox + c;
+        if (gy >= 0 && gy < ha && gx >= 0 && gx < wa) {
+          v[u] = *(const uint4*)&p.y[(size_t)gy * wa + gx];
+          dst[u] = &w.y[r * kWinLP + c];
+        }
+      } else if (k < n) {
+        const int kc = k - nl, pl = kc >= ncl, kk = kc - pl * ncl;
+        const int r = (r0 >> 1) + kk / ncc, c = (c0 >> 1) + (kk % ncc) * 8;
+        const int gy = coy + r, gx = cox + c;
+        if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
+          v[u] = *(const uint4*)&pick(p, 1 + pl)[(size_t)gy * cw + gx];
+          dst[u] = &(pl ? w.v : w.u)[r * kWinCP + c];
+        }
+      }
     }
+#pragma unroll
+    for (int u = 0; u < kWinUnroll; u++)
+      if (dst[u]) *(uint4*)dst[u] = bias4(v[u]);
   }
 }
 

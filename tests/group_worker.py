@@ -29,6 +29,16 @@ import cairo_amd  # noqa: E402
 from oracle import oracle as orc  # noqa: E402
 
 
+def payload_bits(out, ctx, ring, tk):
+    """The frame's payload from its feed (or planes), as a bit array."""
+    if out.feed_status == cairo_amd.FEED_VALID:
+        data, n = cairo_amd.serialize_feed(out.feed, out.feed_bits)
+    else:
+        cy, cu, cv = (out.coef_y, out.coef_u, out.coef_v) if out.coef_y is not None else ctx.fetch_coef(tk)
+        data, n = cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, cy, cu, cv)
+    return np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[:n]
+
+
 def table_mismatch(a, b):
     return [f for f in a.dtype.names if f != "pad" and not np.array_equal(a[f], b[f])]
 
@@ -41,8 +51,10 @@ def oracle_stream(w, h, ring, q, frames, intra_every):
         intra = t == 0 or (intra_every and t % intra_every == 0)
         if intra:
             e.insert_intra()
-        e.encode(orc.make_frame(w, h, t))
-        ref.append((intra, e.block_table(), e.planes(1)))
+        data, n = e.encode(orc.make_frame(w, h, t))
+        head = (14 * 8 if t == 0 else 0) + 10 * 8  # header + frame descriptor precede the payload
+        bits = np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[head:n]
+        ref.append((intra, e.block_table(), e.planes(1), bits))
     final = {t: e.planes(2 + t % ring) for t in range(max(0, frames - ring), frames)}
     return ref, final
 
@@ -60,6 +72,8 @@ def main():
     ap.add_argument("--frames", type=int, default=12)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--intra-every", type=int, default=0)
+    ap.add_argument("--feed", action="store_true", help="members hand over GPU-precoded feeds (bench's mode); "
+                                                         "payloads are checked too")
     a = ap.parse_args()
     w, h, ring, q, F, N = a.w, a.h, a.ring, a.q, a.frames, a.members
     ref, final = oracle_stream(w, h, ring, q, F, a.intra_every)
@@ -85,6 +99,8 @@ def main():
         dist.init_process_group("gloo", init_method=f"file://{a.store}", rank=a.rank, world_size=N)
         ctx = cairo_amd.Context(w, h, ring)
         ctx.set_batch(a.batch)
+        if a.feed:
+            ctx.set_outputs(cairo_amd.OUT_FEED)
         ctx.set_workgroups(max(1, ctx.max_workgroups() // N))  # N members share the device
         recs = [None] * N
         dist.all_gather_object(recs, ctx.peer_info(cross_device=True))
@@ -96,8 +112,12 @@ def main():
         ctx.flush()
         for t in mine:
             out = ctx.wait(tk[t])
-            if table_mismatch(out.table, ref[t][1]) or any(
-                    not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
+            if table_mismatch(out.table, ref[t][1]):
+                bad.append(t)
+            elif a.feed:
+                if not np.array_equal(payload_bits(out, ctx, ring, tk[t]), ref[t][3]):
+                    bad.append(f"payload {t}")
+            elif any(not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
                 bad.append(t)
             ctx.release(tk[t])
         S = -(-ring // N)

@@ -45,14 +45,18 @@ def test_group_4k_in_process():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
 
 
-def test_group_cross_process(tmp_path):
-    """Two processes, one member each, on one device: buffers shared through
-    IPC handles (fine-grained memory, system-scope hand-offs: the cross-GPU
-    code path), records exchanged over gloo."""
+@pytest.mark.parametrize("members,feed,frames", [(2, False, 12), (2, True, 12), (3, True, 12)])
+def test_group_cross_process(tmp_path, members, feed, frames):
+    """One process per member on one device: buffers shared through IPC
+    handles (fine-grained memory, system-scope hand-offs: the cross-GPU code
+    path), records exchanged over gloo; with feed, the members hand over
+    GPU-precoded feeds as bench.py's single-stream leg does, and every
+    frame's payload is checked against the oracle's."""
     store = tmp_path / "store"
-    procs = [subprocess.Popen([sys.executable, WORKER, "xproc", "--members", "2", "--rank", str(k), "--store",
-                               str(store), "--frames", "12", "--batch", "3"], cwd=ROOT, stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for k in range(2)]
+    extra = ["--feed"] if feed else []
+    procs = [subprocess.Popen([sys.executable, WORKER, "xproc", "--members", str(members), "--rank", str(k), "--store",
+                               str(store), "--frames", str(frames), "--batch", "3"] + extra, cwd=ROOT,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for k in range(members)]
     outs = []
     for p in procs:
         try:

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for i in $(seq 1 $N); do
   for v in $(cd build/ab && ls *.so | sed 's/\.so$//'); do
     cp build/ab/$v.so cairo_amd/_lib/libcairo_amd.so
-    timeout -k 10 300 python -u bench.py --config $C --no-cpu-baseline --no-end-to-end "$@" > gpurun_out/ab_${C}_${v}_$i.log 2>&1
+    timeout -k 10 300 python -u bench.py --config $C --no-cpu-baseline --no-end-to-end --no-api "$@" > gpurun_out/ab_${C}_${v}_$i.log 2>&1
     echo "$v $i $(tail -1 gpurun_out/ab_${C}_${v}_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"])')"
   done
 done
