@@ -2,7 +2,7 @@
 3840x2160 p-frames, quality 1..31, VAQ on, one MI355X).
 
 Per quality q, on the band4 content (seed 1234), ring R = 4:
-  * hot-path throughput: `--frames` P-frames after 8 warm-up frames, inputs
+  * hot-path throughput: `--frames` P-frames after 16 warm-up frames, inputs
     resident in HBM, timed like bench.py (Mpix/s);
   * rate: payload bits per P-frame through the native frame pipeline (host
     entropy), plus the 10-byte frame descriptor the encoder writes per frame;
@@ -34,7 +34,7 @@ def psnr(a, b):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="4k", choices=sorted(bench.CONFIGS))
-    ap.add_argument("--frames", type=int, default=48, help="timed P-frames per quality")
+    ap.add_argument("--frames", type=int, default=160, help="timed P-frames per quality")
     ap.add_argument("--q", default="1,2,4,8,12,16,20,24,28,31")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rd_sweep.json"))
     a = ap.parse_args()
@@ -44,7 +44,7 @@ def main():
 
     w, h, ring, _, _ = bench.CONFIGS[a.config]
     ring = 4
-    warm = 8
+    warm = 16
     n = warm + a.frames
     host = np.empty((n, h, w, 3), np.uint8)
     for f in range(n):
@@ -59,11 +59,12 @@ def main():
     for q in [int(x) for x in a.q.split(",")]:
         # throughput (hot path)
         ctx = cairo_amd.Context(w, h, ring)
-        stages = ctx.L.cairo_ctx_stages(ctx.h)
-        bench.run_hot_path(ctx, frames, ptr, 0, warm, q, stages)
+        ctx.set_outputs(cairo_amd.OUT_FEED)  # as bench.py's timed context
+        stages = ctx.stages
+        bench.run_hot_path(ctx, ptr, 0, warm, q, stages)
         ctx.sync()
         t0 = time.perf_counter()
-        bench.run_hot_path(ctx, frames, ptr, warm, a.frames, q, stages)
+        bench.run_hot_path(ctx, ptr, warm, a.frames, q, stages)
         ctx.sync()
         el = time.perf_counter() - t0
         ctx.close()
