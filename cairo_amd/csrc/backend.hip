@@ -1041,7 +1041,9 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
   c->gsize = size;
   c->grank = rank;
   c->gbase = c->next_ticket;
-  c->sys = sys;
+  // (CAIRO_GROUP_FORCE_SYS: system-scope hand-offs in one process too, to
+  // time their cost on one device)
+  c->sys = sys || getenv("CAIRO_GROUP_FORCE_SYS") != nullptr;
   CK(hipMalloc(&c->zero, c->plane_elems * 2));
   CK(hipMemset(c->zero, 0, c->plane_elems * 2));
   // a member's consecutive frames are N stream frames apart
