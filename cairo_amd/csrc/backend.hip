@@ -952,10 +952,16 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
     const size_t S = (size_t)c->stages;
     int16_t *ring = nullptr, *coef = nullptr;
     uint64_t* prog = nullptr;
-    CK(hipExtMallocWithFlags((void**)&ring, c->plane_elems * 2 * c->ring, hipDeviceMallocFinegrained));
-    CK(hipExtMallocWithFlags((void**)&coef, c->plane_elems * 2 * S, hipDeviceMallocFinegrained));
-    CK(hipExtMallocWithFlags((void**)&prog, (size_t)c->hmb * sizeof(uint64_t) * S, hipDeviceMallocFinegrained));
-    CK(hipDeviceSynchronize());
+    hipError_t e = hipExtMallocWithFlags((void**)&ring, c->plane_elems * 2 * c->ring, hipDeviceMallocFinegrained);
+    if (e == hipSuccess) e = hipExtMallocWithFlags((void**)&coef, c->plane_elems * 2 * S, hipDeviceMallocFinegrained);
+    if (e == hipSuccess)
+      e = hipExtMallocWithFlags((void**)&prog, (size_t)c->hmb * sizeof(uint64_t) * S, hipDeviceMallocFinegrained);
+    if (e != hipSuccess) {
+      for (void* q : {(void*)ring, (void*)coef, (void*)prog}) (void)hipFree(q);
+      return fail(e, "hipExtMallocWithFlags(fine-grained)");
+    }
+    int r0 = sync_all(c);  // nothing is in flight (fresh), but the zeroing memsets may be
+    if (r0) return r0;
     (void)hipFree(c->ring_buf);
     (void)hipFree(c->coef);
     (void)hipFree(c->progress);
