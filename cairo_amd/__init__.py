@@ -207,7 +207,7 @@ def _view(addr: int, dtype, count: int) -> np.ndarray:
 class Context:
     """The encode-path backend (``cairo_ctx_*``): one encoder's device state."""
 
-    def __init__(self, width: int, height: int, ring: int = 4, device: int = 0, stages: int = 64):
+    def __init__(self, width: int, height: int, ring: int = 4, device: int = 0, stages: int = 96):
         self.L = lib()
         self.width, self.height, self.ring, self.device = width, height, ring, device
         self.wa, self.ha = (width + 15) & ~15, (height + 15) & ~15
@@ -397,7 +397,7 @@ class Group:
     member n % N (include/cairo_amd.h).  Processes that each own
     one member exchange Context.peer_info() records themselves."""
 
-    def __init__(self, width: int, height: int, ring: int, devices, stages: int = 64, batch: int = 0):
+    def __init__(self, width: int, height: int, ring: int, devices, stages: int = 96, batch: int = 0):
         self.members = [Context(width, height, ring, device=d, stages=stages) for d in devices]
         n = len(self.members)
         per_dev = {d: list(devices).count(d) for d in devices}

@@ -38,17 +38,21 @@ using namespace cairo;
 
 namespace {
 
-constexpr int kDefaultStages = 64;  // staging slots (frames in flight): two 32-frame or four 16-frame batches
+// staging slots (frames in flight): three 32-frame batches, so that the host
+// entropy of one batch overlaps the GPU work of the next two
+constexpr int kDefaultStages = 96;
 constexpr int kMaxStages = 256;
 constexpr int kLaunchSlots = 64;    // per-launch host records (frame views, timing events), reused round-robin
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
-// Frames per launch by default, from measured sweeps (tools/batch_sweep.sh):
-// 32 for frames up to 720p (launch boundaries cost a visible share there),
-// 12 up to about 1080p (+8 % over 16: 2850 vs 2635 Mpix/s), 16 above (4K: 12
-// and 20 both lose 2-3 %, 32 loses 20 %).
-constexpr int kSmallFrameMBs = 4000, kMidFrameMBs = 16000;
+// Frames per launch by default, from measured sweeps (DESIGN.md §4.2,
+// tools/batch_sweep.sh).  With the pools shared between consecutive launches
+// (k_engine next_task) a batch's tail no longer idles half the workers, so
+// larger batches pay: 32 up to about 1080p (1080p: 2981 at 12, 3460 at 24,
+// 3551 at 32 Mpix/s), 24 above (4K: 3868 at 20, 4021-4030 at 24, 4035 at 28,
+// 3974 at 32).
+constexpr int kMidFrameMBs = 16000;
 inline int default_batch(size_t mbs) {
-  return mbs <= (size_t)kSmallFrameMBs ? 32 : mbs <= (size_t)kMidFrameMBs ? 12 : 16;
+  return mbs <= (size_t)kMidFrameMBs ? 32 : 24;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)
@@ -98,7 +102,13 @@ struct cairo_ctx {
   hipStream_t ks = nullptr, cs = nullptr;
   hipStream_t ks2 = nullptr;         // launches alternate between ks and ks2 (consecutive batches overlap)
   hipEvent_t engine_done = nullptr;  // last launched batch finished (copy stream waits on it)
-  hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k
+  hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k (every task done)
+  hipEvent_t batch_ready[kSyncAreas] = {};  // its frames converted, views and sync area set up
+  // the last launch, whose remaining tasks the next launch's workers take first
+  const FrameArgs* prev_fa = nullptr;
+  const int32_t* prev_order = nullptr;
+  int32_t* prev_sync = nullptr;
+  int prev_total = 0, prev_area = 0, prev_decode = 0;
   long long batches = 0;             // launches so far
   // per-slot device buffers
   int16_t *src = nullptr, *coef = nullptr;
@@ -277,6 +287,8 @@ void free_ctx(cairo_ctx* c) {
   if (c->t_base) (void)hipEventDestroy(c->t_base);
   for (auto& ev : c->batch_end)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->batch_ready)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
   if (c->feed_host) (void)hipHostFree(c->feed_host);
   if (c->fs) (void)hipStreamDestroy(c->fs);
@@ -317,6 +329,7 @@ int zero_state(cairo_ctx* c) {
   c->epoch = 0;
   c->last_slot = -1;
   c->batches = 0;
+  c->prev_total = 0;  // its sync areas are zero now
   c->fresh = true;  // the first frame after a reset depends on no earlier frame
   for (auto& s : c->st) *s.err = 0;
   return kSuccess;
@@ -365,14 +378,21 @@ int flush(cairo_ctx* c) {
   // workgroup slots (CUs x occupancy, measured at create: 256 x 3 = 768 on a
   // full MI355X), so two launches are always co-resident.  Every row has a
   // coder and a helper (inter search + deblock) living as long as the row:
-  // equal pools.
+  // equal pools.  The pools are shared: launch b's workers take b-1's
+  // remaining tasks first (all of them are older), so b-1's tail is not left
+  // to b-1's own workers; a batch is complete when its finished-task count
+  // says so (k_batch_wait), not when its launch ends.
   const long long b = c->batches++;
   hipStream_t st = (b & 1) ? c->ks2 : c->ks;
   const int area = (int)(b % kSyncAreas);
   e.sync = c->sync + (size_t)area * c->sync_words;
+  e.pfa = c->prev_fa;
+  e.porder = c->prev_order;
+  e.psync = c->prev_sync;
+  e.ptotal = c->prev_decode == e.decode ? c->prev_total : 0;  // a worker runs one kind of task
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
   {  // half of the resident slots per launch, split between the pools
-    const int total = 2 * (c->wg_rows > 0 ? std::min(c->wg_rows, c->max_rows) : c->max_rows);
+    const int total = 2 * (c->wg_rows > 0 ? std::min(c->wg_rows, (c->stamps ? 2 : 1) * c->max_rows) : c->max_rows);
     int nh = c->wg_helpers > 0 ? std::min(c->wg_helpers, total - 1) : total / 2;
     int nr = total - nh;
     e.n_helpers = std::max(1, std::min(nh, rows));
@@ -408,9 +428,22 @@ int flush(cairo_ctx* c) {
   }
   if (tb) CK(hipEventRecord(tb->ev[0], st));
   CK(launch_convert_batch(e, st));
+  CK(hipEventRecord(c->batch_ready[area], st));
+  // the previous batch's tasks, which this launch's workers may run, need its
+  // frames converted and its views and sync area in place
+  if (e.ptotal) CK(hipStreamWaitEvent(st, c->batch_ready[c->prev_area], 0));
   if (tb) CK(hipEventRecord(tb->ev[1], st));
   if (tb) CK(hipEventRecord(tb->ev[2], st));
   CK(launch_engine(e, st));
+  // the launch ends when its workers find no task left; its batch is done
+  // when every task has finished (the next launch's workers may run the last)
+  CK(launch_batch_wait(e.sync, 2 * rows, c->sticky, st));
+  c->prev_fa = fd;
+  c->prev_order = e.order;
+  c->prev_sync = e.sync;
+  c->prev_total = rows;
+  c->prev_area = area;
+  c->prev_decode = e.decode;
   if (tb) {
     CK(hipEventRecord(tb->ev[3], st));
     tb->frames = e.nframes;
@@ -611,6 +644,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipEventCreateWithFlags(&c->engine_done, hipEventDisableTiming));
   TRY(hipEventCreate(&c->t_base));
   for (auto& ev : c->batch_end) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (auto& ev : c->batch_ready) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 #undef TRY
   r = zero_state(c);
   if (r != kSuccess) {
@@ -660,15 +694,17 @@ int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
 
 int cairo_ctx_set_workgroups(cairo_ctx* c, int rows) {
   // more row coders than stay co-resident with the other in-flight launch
-  // would leave tasks to workgroups that never get a slot
-  if (!c || rows < 0 || rows > c->max_rows) return kInvalidArg;
+  // would leave tasks to workgroups that never get a slot.  With the stamp
+  // diagnostics on (set_debug(2), whose caller waits for each batch) one
+  // launch may take every slot.
+  if (!c || rows < 0 || rows > (c->stamps ? 2 : 1) * c->max_rows) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   c->wg_rows = rows;
   return kSuccess;
 }
 
 int cairo_ctx_set_helpers(cairo_ctx* c, int helpers) {
-  if (!c || helpers < 0 || helpers >= 2 * c->max_rows) return kInvalidArg;
+  if (!c || helpers < 0 || helpers >= 2 * (c->stamps ? 2 : 1) * c->max_rows) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   c->wg_helpers = helpers;
   return kSuccess;

@@ -135,6 +135,7 @@ struct SyncLayout {
   static constexpr int kErr = 0;
   static constexpr int kTicketRows = 2;
   static constexpr int kTicketHelpers = 3;
+  static constexpr int kDone = 4;  // finished tasks (helpers + coders) of the batch
   static constexpr int kFlags = 8;
   // per frame j: inter_done[hmb][ng] (tasks finished per group)
   __host__ __device__ static int frame_words(int hmb, int ng) { return hmb * ng; }
@@ -163,6 +164,13 @@ struct EngineArgs {
   const int32_t* order;    // [nframes * hmb] task order of every pool: (frame << 16 | row),
                            // sorted by (row + kOrderSlope * frame, frame)
   int decode;              // the launch decodes (every frame has FrameDesc::decode set)
+  // The previous launch (still running, or done): its remaining tasks come
+  // first for this launch's workers too, so the two co-resident launches
+  // share their pools (ptotal = 0: none).
+  const FrameArgs* pfa;
+  const int32_t* porder;
+  int32_t* psync;
+  int ptotal;
 };
 
 // Frame-row task order of the engine pools.  A task of frame f, row r waits
@@ -176,6 +184,9 @@ hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);
 // The pipelined encode engine: inter search, macroblock rows (intra search,
 // classify, transform, quantize, reconstruct) and in-loop deblock.
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s);
+// Until every task of the batch (sync area `sync`, `tasks` of them, run by
+// this launch or the next) has finished; bounded like every wait.
+hipError_t launch_batch_wait(int32_t* sync, int tasks, int32_t* sticky, hipStream_t s);
 // Engine workgroups resident per CU (occupancy of k_engine: 3 on gfx950).
 hipError_t engine_blocks_per_cu(int* n);
 // Debug: rebuild the pre-deblock reconstruction of frame j of the batch from

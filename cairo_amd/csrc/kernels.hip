@@ -1932,6 +1932,58 @@ __device__ __forceinline__ bool is_helper(int b, int nh, int n) {
   return ((b + 1) * nh) / n > (b * nh) / n;
 }
 
+// The next task of a pool (ticket word tk): from this launch's queue or the
+// previous launch's, whichever task comes first in the task order (row +
+// kOrderSlope * frame; the previous launch's frames come first, so its frame
+// j is this launch's frame j - pframes).  The previous batch's tail thereby
+// interleaves with this batch's first rows as the order says, and every free
+// worker of either launch takes the oldest task: the two co-resident launches
+// share their pools.  Returns the ticket (prev: of the previous launch), or
+// -1 when both queues are exhausted.
+#ifndef CAIRO_SHARE
+#define CAIRO_SHARE 1
+#endif
+__device__ __forceinline__ int next_task(const EngineArgs& e, int tk, int total, EngineLds& L, bool& prev) {
+  const int ptotal = CAIRO_SHARE ? e.ptotal : 0;
+  if (threadIdx.x == 0) {
+    const int pframes = ptotal / e.hmb;
+    int q = 0, tt = -1;
+    for (;;) {
+      const int tp = ptotal ? __hip_atomic_load(e.psync + tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      const int tb = __hip_atomic_load(e.sync + tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tp >= ptotal && tb >= total) break;  // both exhausted
+      bool usep = tp < ptotal;
+      if (usep && tb < total) {
+        const int op = e.porder[tp], ob = e.order[tb];
+        usep = (op & 0xFFFF) + kOrderSlope * (op >> 16) <= (ob & 0xFFFF) + kOrderSlope * (pframes + (ob >> 16));
+      }
+      tt = __hip_atomic_fetch_add((usep ? e.psync : e.sync) + tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q = usep;
+      if (tt < (usep ? ptotal : total)) break;  // else taken meanwhile: look again
+      tt = -1;
+    }
+    L.slot = tt;
+    L.flag = q;
+  }
+  __syncthreads();
+  const int t = uni(L.slot);
+  prev = uni(L.flag) != 0;
+  __syncthreads();
+  return t;
+}
+
+// A finished task counts toward its batch's completion (k_batch_wait) once
+// all its stores are visible.
+__device__ __forceinline__ void task_done(int32_t* sync) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(sync + SyncLayout::kDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <bool kDecode>
 __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   __shared__ EngineLds L;
@@ -1947,20 +1999,24 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
     // waves (A/B: 1080p +3 %, 4K +3 %; 720p -1 %, so not there).
     if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(2);
     for (;;) {
-      const int t = dequeue(e.sync + SyncLayout::kTicketHelpers, &L.slot);
+      bool prev;
+      const int t = next_task(e, SyncLayout::kTicketHelpers, total, L, prev);
+      if (t < 0) break;
       trace(e.trace, 0, 1000000 + t);
-      if (t >= total) break;
-      const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
-      row_helper(((FA*)e.fa)[uni(j)], r, L.u.helper, &L.flag, e.trace);
+      const int32_t o = (prev ? e.porder : e.order)[t];
+      row_helper(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.helper, &L.flag, e.trace);
+      task_done(prev ? e.psync : e.sync);
       trace(e.trace, 0, 2000000 + t);
     }
   } else {
     for (;;) {
-      const int t = dequeue(e.sync + SyncLayout::kTicketRows, &L.slot);
+      bool prev;
+      const int t = next_task(e, SyncLayout::kTicketRows, total, L, prev);
+      if (t < 0) break;
       trace(e.trace, 0, 3000000 + t);
-      if (t >= total) break;
-      const int j = e.order[t] >> 16, r = e.order[t] & 0xFFFF;
-      code_row<kDecode>(((FA*)e.fa)[uni(j)], r, L.u.row, e.trace);
+      const int32_t o = (prev ? e.porder : e.order)[t];
+      code_row<kDecode>(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.row, e.trace);
+      task_done(prev ? e.psync : e.sync);
       trace(e.trace, 0, 4000000 + t);
     }
   }
@@ -2028,6 +2084,27 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
 
 hipError_t engine_blocks_per_cu(int* n) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, reinterpret_cast<const void*>(&k_engine<false>), 256, 0);
+}
+
+// One wave: thread 0 polls the batch's finished-task count.
+__global__ __launch_bounds__(64) void k_batch_wait(int32_t* sync, int tasks, int32_t* sticky) {
+  if (threadIdx.x) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(sync + SyncLayout::kDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tasks) {
+    __builtin_amdgcn_s_sleep(8);
+    if (__hip_atomic_load(sync + SyncLayout::kErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+      __hip_atomic_store(sync + SyncLayout::kErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+hipError_t launch_batch_wait(int32_t* sync, int tasks, int32_t* sticky, hipStream_t s) {
+  hipLaunchKernelGGL(k_batch_wait, dim3(1), dim3(64), 0, s, sync, tasks, sticky);
+  return hipGetLastError();
 }
 
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s) {

@@ -63,9 +63,11 @@ typedef struct cairo_frame_result {
 CAIRO_API int cairo_ctx_create(uint32_t width, uint32_t height, uint32_t ring, int device,
                                cairo_ctx **out);
 /* The same with an explicit number of staging slots (frames in flight,
- * 2..256; cairo_ctx_create uses 64).  A synchronous caller (one frame in
- * flight, as evx1_encoder::encode) needs 2: about 0.35 GB of HBM for a 4K
- * R = 4 context instead of 8 GB.  Frames per launch are at most stages / 2. */
+ * 2..256; cairo_ctx_create uses 96: three 32-frame launches, so that the
+ * host entropy of one overlaps the GPU work of the next two).  A synchronous
+ * caller (one frame in flight, as evx1_encoder::encode) needs 2: about
+ * 0.35 GB of HBM for a 4K R = 4 context instead of 12 GB.  Frames per launch
+ * are at most stages / 2. */
 CAIRO_API int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int device,
                                   int stages, cairo_ctx **out);
 CAIRO_API int cairo_ctx_destroy(cairo_ctx *ctx);
@@ -98,7 +100,7 @@ CAIRO_API int cairo_ctx_sync(cairo_ctx *ctx);
 /* Staging slots = frames that may be in flight (submitted, not released). */
 CAIRO_API int cairo_ctx_stages(const cairo_ctx *ctx);
 /* Frames per engine launch, 1..min(32, stages/2) (default 32 for frames of up to
- * 4000 macroblocks, 12 up to 16000, 16 above). */
+ * 16000 macroblocks, 24 above). */
 CAIRO_API int cairo_ctx_set_batch(cairo_ctx *ctx, int frames);
 /* The default frames per launch for a frame size (no device needed; 0 for an
  * empty size). */

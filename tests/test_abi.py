@@ -56,6 +56,6 @@ def test_default_batch(cairo):
     """Frames per launch by frame size (backend.hip default_batch; DESIGN.md §4.2 sweeps)."""
     assert cairo.default_batch(352, 288) == 32
     assert cairo.default_batch(1280, 720) == 32
-    assert cairo.default_batch(1920, 1080) == 12
-    assert cairo.default_batch(3840, 2160) == 16
+    assert cairo.default_batch(1920, 1080) == 32
+    assert cairo.default_batch(3840, 2160) == 24
     assert cairo.default_batch(0, 720) == 0

@@ -23,8 +23,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="720p")
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--rows", type=int, default=0, help="row-coder workgroups (0 = default)")
+ap.add_argument("--helpers", type=int, default=0, help="helper workgroups of the launch (0 = default: half)")
 ap.add_argument("--row", type=int, default=10, help="MB row of the group timeline")
 ap.add_argument("--frame", type=int, default=1, help="frame (>= 1) of the batch for the lag / group-timeline sections")
+ap.add_argument("--dump", default="", help="also save the raw stamps (npz) here")
 a = ap.parse_args()
 w, h, ring, q = CFG[a.config]
 ctx = cairo_amd.Context(w, h, ring)
@@ -32,6 +34,8 @@ ctx.set_debug(2)
 ctx.set_batch(a.batch)
 if a.rows:
     ctx.set_workgroups(a.rows)
+if a.helpers:
+    ctx.set_helpers(a.helpers)
 B = a.batch
 for first in (0, B):  # warm-up batch, measured batch
     frames = [cairo_amd.make_band4(w, h, t) for t in range(first, first + B)]
@@ -40,6 +44,8 @@ for first in (0, B):  # warm-up batch, measured batch
         ctx.wait(t, copy=False)
         ctx.release(t)
 st, dbs, kio, ist = ctx.read_stamps()  # 10 ns ticks
+if a.dump:
+    np.savez_compressed(a.dump, st=st[:B], dbs=dbs[:B], kio=kio, ist=ist[:B])
 dbs = dbs[:B].astype(np.int64)
 ist = ist[:B].astype(np.int64)
 st = st[:B].astype(np.int64)
