@@ -84,6 +84,7 @@ def parse():
                         "or the coefficient planes")
     p.add_argument("--helpers", type=int, default=0, help="helper workgroups of a launch's workers (0 = default)")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
+    p.add_argument("--stages", type=int, default=0, help="staging slots of the timed context (0 = library default)")
     return p.parse_args()
 
 
@@ -236,7 +237,7 @@ def main():
     def frame_ptr(f):
         return base + f * stride
 
-    ctx = share(cairo_amd.Context(w, h, ring, device=local))
+    ctx = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
     ctx.set_batch(batch)
     # what the pipeline and the drop-in encoder hand to the host coder
     ctx.set_outputs(cairo_amd.OUT_FEED if a.outputs == "feed" else cairo_amd.OUT_COEF)
@@ -323,7 +324,7 @@ def main():
     e2e = None
     e2e_records = {}
     if not a.no_end_to_end:
-        ctx2 = share(cairo_amd.Context(w, h, ring, device=local))
+        ctx2 = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
         ctx2.set_batch(batch)
         e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, warm_frames, timed_frames, barrier, dist,
                          dev, world, n_check, e2e_records)
@@ -393,7 +394,7 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
     recs = {}
     ctx = None
     try:
-        ctx = share(cairo_amd.Context(w, h, ring, device=local))
+        ctx = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
         ctx.set_batch(batch)
         ctx.set_outputs(cairo_amd.OUT_FEED)
         peers = [None] * world

@@ -49,7 +49,10 @@ __host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
 }
 
 // Frames per engine launch.
-constexpr int kMaxBatch = 32;
+#ifndef CAIRO_MAX_BATCH
+#define CAIRO_MAX_BATCH 32
+#endif
+constexpr int kMaxBatch = CAIRO_MAX_BATCH;
 // Members of a frame-interleaved group (cairo_ctx_join_group).
 constexpr int kMaxGroup = 16;
 
@@ -177,7 +180,10 @@ struct EngineArgs {
 // at most on frame f-1, row r+3, so any slope > 3 keeps every wait pointing
 // to an earlier key (deadlock-free), while frames interleave in the pools
 // instead of queueing behind each other.
-constexpr int kOrderSlope = 5;
+#ifndef CAIRO_ORDER_SLOPE
+#define CAIRO_ORDER_SLOPE 5
+#endif
+constexpr int kOrderSlope = CAIRO_ORDER_SLOPE;
 
 // RGB -> YUV of every frame of the batch into its slot's source planes.
 hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);

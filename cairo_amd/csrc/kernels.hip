@@ -1115,23 +1115,11 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     const int k = st.k;
     const int c0 = k * kDbChunk, c1 = min(c0 + kDbChunk, a.wa);
     const bool last = k == nch - 1;
-    // ---- inputs of chunk k ----
-    if (r > 0 && tid == 0) {  // rows above final through column c1
-      if (progress_at(&prog[r - 1]) < (above | (uint32_t)c1)) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (progress_at(&prog[r - 1]) < (above | (uint32_t)c1)) {
-          if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    {  // pre-deblock pixels of MB c0/16 of row r (granules) + block info
+    // ---- inputs of chunk k: waves 0-2 the granules of MB k; wave 3 polls
+    //      row r-1's progress (rows above final through column c1), then
+    //      loads the block info and those 4 rows ----
+    const int hb1 = last ? a.wa : c1 - 8, vb1 = last ? a.wa : c1 - 8;
+    {
       const int m = c0 >> 4;
       if (tid < kGranulesPerMB) {
         const uint64_t* gp = gran_mb(a, m, r) + tid;
@@ -1146,67 +1134,85 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
         int16_t* p = db_px(D, pl, row, col);
         p[0] = (int16_t)(d & 0xFFFF);
         p[1] = (int16_t)(d >> 16);
-      } else if (tid < kGranulesPerMB + 2) {
-        const int row = r - 1 + (tid - kGranulesPerMB);
-        int e = 0;
-        if (row >= 0) {
-          const uint64_t* gp = gran_mb(a, m, row) + kGranulesPerMB;
-          e = (int)gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
-        }
-        D.info[tid - kGranulesPerMB][m & 7] = (int16_t)e;
-      } else if (r > 0) {  // 4 final rows above: luma 4 x 8 dwords, chroma 2 x 4 x 4 (sc1)
-        for (int i = tid - kGranulesPerMB - 2; i < 32 + 32; i += 256 - kGranulesPerMB - 2) {
-          int pl, row, col;
-          const int16_t* g;
-          if (i < 32) {
-            pl = 0, row = i >> 3, col = c0 + 2 * (i & 7);
-            g = cs.y + (size_t)(y0 + row) * a.wa + col;
-          } else {
-            const int j = i - 32, pj = j >> 4, jj = j & 15;
-            pl = 1 + pj, row = jj >> 2, col = (c0 >> 1) + 2 * (jj & 3);
-            g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
+      } else {  // wave 3 (uniform loop: every lane reads the same word)
+        if (r > 0 && uni((int)(progress_at(&prog[r - 1]) < (above | (uint32_t)c1)))) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (uni((int)(progress_at(&prog[r - 1]) < (above | (uint32_t)c1)))) {
+            if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+              if (tid == kGranulesPerMB) {
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              break;
+            }
           }
-          const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          int16_t* p = db_px(D, pl, row, col);
-          p[0] = (int16_t)(d & 0xFFFF);
-          p[1] = (int16_t)(d >> 16);
+        }
+        if (tid < kGranulesPerMB + 2) {
+          const int row = r - 1 + (tid - kGranulesPerMB);
+          int e = 0;
+          if (row >= 0) {
+            const uint64_t* gp = gran_mb(a, m, row) + kGranulesPerMB;
+            e = (int)gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
+          }
+          D.info[tid - kGranulesPerMB][m & 7] = (int16_t)e;
+        } else if (r > 0) {  // 4 final rows above: luma 4 x 8 dwords, chroma 2 x 4 x 4 (sc1)
+          for (int i = tid - kGranulesPerMB - 2; i < 32 + 32; i += 256 - kGranulesPerMB - 2) {
+            int pl, row, col;
+            const int16_t* g;
+            if (i < 32) {
+              pl = 0, row = i >> 3, col = c0 + 2 * (i & 7);
+              g = cs.y + (size_t)(y0 + row) * a.wa + col;
+            } else {
+              const int j = i - 32, pj = j >> 4, jj = j & 15;
+              pl = 1 + pj, row = jj >> 2, col = (c0 >> 1) + 2 * (jj & 3);
+              g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
+            }
+            const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int16_t* p = db_px(D, pl, row, col);
+            p[0] = (int16_t)(d & 0xFFFF);
+            p[1] = (int16_t)(d >> 16);
+          }
         }
       }
     }
     __syncthreads();
-    // ---- band A: H edges of [c0, c1) (luma 16 + 2 x 8 chroma columns) ----
-    if (r > 0 && tid < 32) {
-      if (tid < 16) {
-        const int col = c0 + tid;
-        db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
-      } else {
-        const int pl = 1 + ((tid - 16) >> 3), col = (c0 >> 1) + (tid & 7);
-        db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
+    // ---- the filters, in order, by wave 0 alone: a wave's LDS accesses
+    //      execute in order, so no workgroup barrier between the steps ----
+    if (tid < 64) {
+      const int lane = tid;
+      // band A H edges of [c0, c1): luma 16 columns (lanes 0-15), chroma 2 x 8 (16-31)
+      if (r > 0 && lane < 32) {
+        if (lane < 16) {
+          const int col = c0 + lane;
+          db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
+        } else {
+          const int pl = 1 + ((lane - 16) >> 3), col = (c0 >> 1) + (lane & 7);
+          db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
+        }
       }
-    }
-    __syncthreads();
-    // ---- band A: V edges of units c0, c0+8 (luma) and c0/2 (chroma) ----
-    if (tid < 32) {
-      if (tid < 16) {
-        const int x = c0 + 8 * (tid >> 3), row = 4 + (tid & 7);
+      __builtin_amdgcn_wave_barrier();
+      // band A V edges of units c0, c0+8 (luma) and c0/2 (chroma)
+      if (lane < 16) {
+        const int x = c0 + 8 * (lane >> 3), row = 4 + (lane & 7);
         if (x > 0 && x < c1)
           db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
-      } else {
-        const int pl = 1 + ((tid - 16) >> 3), x = c0 >> 1, row = 4 + (tid & 7);
+      } else if (lane < 32) {
+        const int pl = 1 + ((lane - 16) >> 3), x = c0 >> 1, row = 4 + (lane & 7);
         if (x > 0)
           db_line(D, pl, false, row, x - 4, D.info[1][((x - 1) >> 3) & 7], D.info[1][(x >> 3) & 7]);
       }
-    }
-    __syncthreads();
-    // ---- band B: H edges of [hb0, hb1), then V edges of units [vb0, vb1) ----
-    const int hb1 = last ? a.wa : c1 - 8, vb1 = last ? a.wa : c1 - 8;
-    for (int col = hb0 + tid; col < hb1; col += 256)
-      db_line(D, 0, true, 8, col, D.info[1][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
-    __syncthreads();
-    for (int i = tid; i < 8 * ((vb1 - vb0 + 7) >> 3); i += 256) {
-      const int x = vb0 + 8 * (i >> 3), row = 12 + (i & 7);
-      if (x < vb1) db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
+      __builtin_amdgcn_wave_barrier();
+      // band B H edges of [hb0, hb1), then V edges of units [vb0, vb1)
+      for (int col = hb0 + lane; col < hb1; col += 64)
+        db_line(D, 0, true, 8, col, D.info[1][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < 8 * ((vb1 - vb0 + 7) >> 3); i += 64) {
+        const int x = vb0 + 8 * (i >> 3), row = 12 + (i & 7);
+        if (x < vb1) db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
+      }
     }
     __syncthreads();
     hb0 = max(hb0, hb1);
