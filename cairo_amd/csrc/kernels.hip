@@ -772,17 +772,25 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     __syncthreads();
     if (is && off == 1) is[4] = __builtin_amdgcn_s_memrealtime();
     bool lvl2c = false, lvl2r = false;  // workgroup-uniform
+    bool lvl2_open = true;  // workgroup-uniform: some wave's search may still leave level 1
     // steps 16, 8, 4, 2, 1, then the sub-pel step (reach 1 around the best)
     for (int si = 0; si < 6; si++) {
       const int step = si < 5 ? kRadius >> si : 1;
-      if (!lvl2r) {
+      if (!lvl2r && lvl2_open) {
         // this wave's candidates of the step reach window rows by+step-oy+15
-        // and columns bx+step-ox+15 at most
+        // and columns bx+step-ox+15 at most; those of every remaining step
+        // (reach rem = step + step/2 + ... + 1 + the sub-pel 1) no further
+        // than by+rem-oy+15: once no wave can leave level 1 any more, the
+        // waves run their remaining steps without workgroup barriers
+        const int rem = si < 5 ? 2 * step : 1;
         const int want = need ? (s.by + step - oy > kLvl1Rows - kMB) * 2 + (!lvl2c && s.bx + step - ox > kLvl1Cols - kMB)
                               : 0;
-        if ((threadIdx.x & 63) == 0) L.lvl2[si][wave] = want;
+        const int may = need && (s.by + rem - oy > kLvl1Rows - kMB || (!lvl2c && s.bx + rem - ox > kLvl1Cols - kMB));
+        if ((threadIdx.x & 63) == 0) L.lvl2[si][wave] = want | (may << 2);
         __syncthreads();
-        const int m = L.lvl2[si][0] | L.lvl2[si][1] | L.lvl2[si][2] | L.lvl2[si][3];
+        const int m4 = L.lvl2[si][0] | L.lvl2[si][1] | L.lvl2[si][2] | L.lvl2[si][3];
+        const int m = m4 & 3;
+        lvl2_open = (m4 >> 2) != 0;
         if (m) {
           if (is) is[5] = __builtin_amdgcn_s_memrealtime();
           helper_wait(a, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2), D, st, flag);
