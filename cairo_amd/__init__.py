@@ -92,6 +92,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_set_helpers": (I, [P, I]),
         "cairo_ctx_max_workgroups": (I, [P]),
         "cairo_default_batch": (I, [U, U]),
+        "cairo_task_order": (I, [I, I, P, ctypes.POINTER(I)]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "cairo_serialize_feed": (I, [P, ctypes.c_uint64, P, U, ctypes.POINTER(U)]),
@@ -440,6 +441,15 @@ class Group:
 def default_batch(width: int, height: int) -> int:
     """Frames per engine launch the library uses by default for this frame size."""
     return int(lib().cairo_default_batch(width, height))
+
+
+def task_order(hmb: int, frames: int):
+    """-> (the engine's task order of a launch: int32 (frame << 16 | row) per
+    task, the order slope)."""
+    out = np.zeros(frames * hmb, np.int32)
+    slope = ctypes.c_int()
+    _ck(lib().cairo_task_order(hmb, frames, _ptr(out), ctypes.byref(slope)), "cairo_task_order")
+    return out, slope.value
 
 
 def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):

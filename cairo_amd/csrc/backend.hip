@@ -109,6 +109,7 @@ struct cairo_ctx {
   const int32_t* prev_order = nullptr;
   int32_t* prev_sync = nullptr;
   int prev_total = 0, prev_area = 0, prev_decode = 0;
+  int order_slope = kOrderSlope;  // of the task order tables (3N + 2 in an N-member group)
   long long batches = 0;             // launches so far
   // per-slot device buffers
   int16_t *src = nullptr, *coef = nullptr;
@@ -390,6 +391,7 @@ int flush(cairo_ctx* c) {
   e.porder = c->prev_order;
   e.psync = c->prev_sync;
   e.ptotal = c->prev_decode == e.decode ? c->prev_total : 0;  // a worker runs one kind of task
+  e.slope = c->order_slope;
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
   {  // half of the resident slots per launch, split between the pools
     const int total = 2 * (c->wg_rows > 0 ? std::min(c->wg_rows, (c->stamps ? 2 : 1) * c->max_rows) : c->max_rows);
@@ -670,6 +672,7 @@ int cairo_ctx_reset(cairo_ctx* c) {
   for (auto& s : c->st) s.busy = false;
   if (c->gsize > 1) {  // a reset leaves the group (its members reset and rejoin together)
     leave_group(c);
+    c->order_slope = kOrderSlope;
     const std::vector<int32_t> ord = task_order((int)c->hmb, kOrderSlope);
     CK(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
@@ -681,6 +684,14 @@ int cairo_ctx_stages(const cairo_ctx* c) { return c ? c->stages : 0; }
 int cairo_default_batch(uint32_t width, uint32_t height) {
   if (!width || !height) return 0;
   return default_batch((size_t)((width + 15) / 16) * ((height + 15) / 16));
+}
+
+int cairo_task_order(int hmb, int frames, int32_t* out, int* slope) {
+  if (hmb < 1 || hmb > 0xFFFF || frames < 1 || frames > kMaxBatch || !out) return kInvalidArg;
+  const std::vector<int32_t> ord = task_order(hmb, kOrderSlope);
+  memcpy(out, &ord[(size_t)(frames - 1) * kMaxBatch * hmb], (size_t)frames * hmb * sizeof(int32_t));
+  if (slope) *slope = kOrderSlope;
+  return kSuccess;
 }
 
 int cairo_ctx_set_batch(cairo_ctx* c, int frames) {
@@ -1089,8 +1100,10 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
   CK(hipMalloc(&c->zero, c->plane_elems * 2));
   CK(hipMemset(c->zero, 0, c->plane_elems * 2));
   // a member's consecutive frames are N stream frames apart
-  const std::vector<int32_t> ord = task_order((int)c->hmb, 3 * size + 2);
+  c->order_slope = 3 * size + 2;
+  const std::vector<int32_t> ord = task_order((int)c->hmb, c->order_slope);
   CK(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->prev_total = 0;  // the previous launch's queue used the other order
   return kSuccess;
 }
 

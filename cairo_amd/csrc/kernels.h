@@ -174,6 +174,7 @@ struct EngineArgs {
   const int32_t* porder;
   int32_t* psync;
   int ptotal;
+  int slope;               // of both task orders (kOrderSlope; 3N + 2 for a member of an N-GPU group)
 };
 
 // Frame-row task order of the engine pools.  A task of frame f, row r waits

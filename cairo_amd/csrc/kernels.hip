@@ -1948,7 +1948,7 @@ __device__ __forceinline__ bool is_helper(int b, int nh, int n) {
 
 // The next task of a pool (ticket word tk): from this launch's queue or the
 // previous launch's, whichever task comes first in the task order (row +
-// kOrderSlope * frame; the previous launch's frames come first, so its frame
+// e.slope * frame; the previous launch's frames come first, so its frame
 // j is this launch's frame j - pframes).  The previous batch's tail thereby
 // interleaves with this batch's first rows as the order says, and every free
 // worker of either launch takes the oldest task: the two co-resident launches
@@ -1969,7 +1969,7 @@ __device__ __forceinline__ int next_task(const EngineArgs& e, int tk, int total,
       bool usep = tp < ptotal;
       if (usep && tb < total) {
         const int op = e.porder[tp], ob = e.order[tb];
-        usep = (op & 0xFFFF) + kOrderSlope * (op >> 16) <= (ob & 0xFFFF) + kOrderSlope * (pframes + (ob >> 16));
+        usep = (op & 0xFFFF) + e.slope * (op >> 16) <= (ob & 0xFFFF) + e.slope * (pframes + (ob >> 16));
       }
       tt = __hip_atomic_fetch_add((usep ? e.psync : e.sync) + tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       q = usep;

@@ -105,6 +105,12 @@ CAIRO_API int cairo_ctx_set_batch(cairo_ctx *ctx, int frames);
 /* The default frames per launch for a frame size (no device needed; 0 for an
  * empty size). */
 CAIRO_API int cairo_default_batch(uint32_t width, uint32_t height);
+/* The engine's (frame, row) task order for a launch of `frames` frames of hmb
+ * macroblock rows: frames * hmb words (frame << 16 | row), sorted by row +
+ * slope * frame; *slope receives the slope.  A launch's workers also take the
+ * previous launch's tasks, merged by the same key with that launch's frames
+ * first (no device needed; for tests of the deadlock-freedom argument). */
+CAIRO_API int cairo_task_order(int hmb, int frames, int32_t *out, int *slope);
 
 /* Introspection (synchronous; of the last submitted frame).  which: 0 input,
  * 1 output_cache, 2+k ring slot k. */
