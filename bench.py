@@ -189,6 +189,14 @@ def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None):
         retire()
 
 
+T_START = time.perf_counter()
+
+
+def note(rank, msg):
+    """Progress on stderr (the JSON line stays the only stdout line)."""
+    print(f"[bench rank {rank} +{time.perf_counter() - T_START:.0f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,6 +241,7 @@ def main():
             frames[c0:c0 + n].copy_(torch.from_numpy(host))
     torch.cuda.synchronize()
     base, stride = frames.data_ptr(), w * h * 3
+    note(rank, f"{nframes} {w}x{h} frames resident in HBM")
 
     def frame_ptr(f):
         return base + f * stride
@@ -265,6 +274,7 @@ def main():
     # warmup: frame 0 (I) + P-frames, in the same context and launches as the timed region
     run_hot_path(ctx, frame_ptr, 0, warm_frames, q, stages, keep_record)
     ctx.sync()
+    note(rank, "warm-up done")
     ctx.set_profiling(True)
     ctx.take_timings()
     barrier()
@@ -278,6 +288,7 @@ def main():
     ctx.set_profiling(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
     value = aggregate_mpix(w, h, timed_frames, world, elapsed)
+    note(rank, f"timed region: {timed_frames} frames in {elapsed:.3f} s")
     kf = max(kframes, 1)
     abytes = algorithmic_bytes(w, h, ring)
     engine_busy_ms = kernel_ms[3] / kf  # union of the launch intervals / frames
@@ -324,6 +335,7 @@ def main():
     e2e = None
     e2e_records = {}
     if not a.no_end_to_end:
+        note(rank, "end-to-end leg")
         ctx2 = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
         ctx2.set_batch(batch)
         e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, warm_frames, timed_frames, barrier, dist,
@@ -332,6 +344,7 @@ def main():
     ctx.close()
     single = None
     if world > 1 and not a.no_single_stream:
+        note(rank, "single-stream leg")
         single = single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm_frames, timed_frames, barrier,
                                dist, dev, world, rank, local, share)
     del frames
@@ -339,6 +352,7 @@ def main():
 
     api = None
     if rank == 0 and world == 1 and not a.no_api:
+        note(rank, "encode() API leg")
         api = api_encode(w, h, ring, q, 2 + max(4, min(12, int(100e6 / (w * h)))))
 
     result = {
@@ -367,6 +381,7 @@ def main():
         "single_stream": single,
     }
     if check:
+        note(rank, "CPU baseline and bit-exact check")
         result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, n_check - 1,
                                                                    hot_records, e2e_records)
     else:
@@ -393,48 +408,72 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
     n_check = 4
     recs = {}
     ctx = None
-    try:
-        ctx = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
+    state = {"err": ""}
+
+    def step(what, fn):
+        """Run fn unless a rank already failed, then agree on failure: every
+        rank makes the same collective calls whatever happened (a rank that
+        failed must not leave the others in a barrier)."""
+        if not state["err"]:
+            try:
+                fn()
+            except Exception as ex:  # noqa: BLE001 -- reported in the line
+                state["err"] = f"rank {rank} ({what}): {type(ex).__name__}: {ex}"[:300]
+                note(rank, f"single stream failed: {state['err']}")
+        bad = torch.tensor([1.0 if state["err"] else 0.0], dtype=torch.float64)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=gloo)
+        if bad.item() and not state["err"]:
+            state["err"] = f"rank {rank}: stopped ({what}): another rank failed"
+        return not state["err"]
+
+    def run(first, count, keep):
+        inflight = deque()
+
+        def retire():
+            n, t = inflight.popleft()
+            out = ctx.wait(t, copy=False)
+            if keep and n < n_check:
+                recs[n] = record(cairo_amd, w, h, ring, q, n, *payload(cairo_amd, ctx, out, t))
+            ctx.release(t)
+
+        for n in range(first, first + count):
+            if n % world != rank:
+                continue
+            if len(inflight) == ctx.stages:
+                retire()
+            inflight.append((n, ctx.submit(frame_ptr(n), n, n > 0, q, on_device=True)))
+        ctx.flush()
+        while inflight:
+            retire()
+        ctx.sync()
+
+    def make():
+        nonlocal ctx
+        # two launches' worth of staging slots: every member imports the
+        # others' output_cache slots over IPC, so they are kept small
+        ctx = share(cairo_amd.Context(w, h, ring, device=local, stages=a.stages or 2 * batch))
         ctx.set_batch(batch)
         ctx.set_outputs(cairo_amd.OUT_FEED)
-        peers = [None] * world
-        dist.all_gather_object(peers, ctx.peer_info(cross_device=True), group=gloo)
-        ctx.join_group(rank, peers)
-        stages = ctx.stages
 
-        def run(first, count, keep):
-            inflight = deque()
-
-            def retire():
-                n, t = inflight.popleft()
-                out = ctx.wait(t, copy=False)
-                if keep and n < n_check:
-                    recs[n] = record(cairo_amd, w, h, ring, q, n, *payload(cairo_amd, ctx, out, t))
-                ctx.release(t)
-
-            for n in range(first, first + count):
-                if n % world != rank:
-                    continue
-                if len(inflight) == stages:
-                    retire()
-                inflight.append((n, ctx.submit(frame_ptr(n), n, n > 0, q, on_device=True)))
-            ctx.flush()
-            while inflight:
-                retire()
-
-        dist.barrier(group=gloo)  # in-kernel waits on other ranks' frames are bounded (2 s): start together
-        run(0, warm, True)
-        ctx.sync()
-        dist.barrier(group=gloo)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        run(warm, timed, False)
-        ctx.sync()
-        el = time.perf_counter() - t0
-        dist.barrier(group=gloo)
-        res = el
-    except Exception as ex:  # noqa: BLE001 -- reported in the line
-        err = f"rank {rank}: {type(ex).__name__}: {ex}"[:300]
+    info = {}
+    step("context", make)
+    note(rank, "single stream: context made")
+    step("peer info", lambda: info.update(rec=ctx.peer_info(cross_device=True)))
+    note(rank, "single stream: peer info")
+    peers = [None] * world
+    dist.all_gather_object(peers, info.get("rec"), group=gloo)
+    note(rank, "single stream: peers gathered")
+    # in-kernel waits on other ranks' frames are bounded (2 s): ranks start each phase together
+    if step("join", lambda: ctx.join_group(rank, peers)):
+        note(rank, "single stream: group joined")
+    if step("warm-up", lambda: run(0, warm, True)):
+        note(rank, "single stream: warm-up done")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if step("timed", lambda: run(warm, timed, False)):
+        res = time.perf_counter() - t0
+        note(rank, "single stream: timed run done")
+    err = state["err"]
     ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=gloo)
     elt = torch.tensor([res or 0.0], dtype=torch.float64)

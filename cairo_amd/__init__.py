@@ -398,7 +398,7 @@ class Group:
     member n % N (include/cairo_amd.h).  Processes that each own
     one member exchange Context.peer_info() records themselves."""
 
-    def __init__(self, width: int, height: int, ring: int, devices, stages: int = 96, batch: int = 0):
+    def __init__(self, width: int, height: int, ring: int, devices, stages: int = 64, batch: int = 0):
         self.members = [Context(width, height, ring, device=d, stages=stages) for d in devices]
         n = len(self.members)
         per_dev = {d: list(devices).count(d) for d in devices}

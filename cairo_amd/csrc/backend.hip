@@ -993,6 +993,14 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->fresh || c->npend || c->gsize > 1) return kInvalidResource;  // before any frame, outside a group
   CK(hipSetDevice(c->device));
+  // Importing an IPC buffer of 2 GiB or more never returned on the test
+  // boxes (a 4K context with 96 staging slots exports 2.4 GB of
+  // output_cache): refuse instead; a group member needs few staging slots.
+  if (cross_device && c->plane_elems * 2 * (size_t)c->stages >= (size_t(1) << 31)) {
+    fprintf(stderr, "[cairo_amd] peer_info: %d staging slots export %.2f GB of output_cache; IPC imports need < 2 GiB "
+                    "(create the member with fewer stages)\n", c->stages, c->plane_elems * 2.0 * c->stages / 1e9);
+    return kInvalidArg;
+  }
   if (cross_device && !c->fine_grained) {
     // Memory another device reads while this one writes it: fine-grained, so
     // that system-scope releases and acquires order it across devices.

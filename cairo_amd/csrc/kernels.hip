@@ -1540,6 +1540,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
       trace(tr, 1, bx);
+      trace(tr, 2, (int)a.epoch * 1000 + by);
       stamp(a, mb, 0);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
       if ((bx & 3) == 0) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
@@ -1887,6 +1888,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
   DbState st{0, 0, 0, 8};
   for (int g = 0; g < a.ng; g++) {
     trace(tr, 1, g);
+    trace(tr, 2, (int)a.epoch * 1000 + r);
     uint64_t* is = a.istamps && tid == 0 ? a.istamps + (size_t)(r * a.ng + g) * kIStamps : nullptr;
     if (is) is[0] = __builtin_amdgcn_s_memrealtime(), is[3] = is[4] = is[5] = is[6] = is[7] = is[8] = is[9] = is[10] = 0;
     // level 1 of the group's window (inter_task); deblock meanwhile
@@ -1910,10 +1912,10 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
   }
   trace(tr, 1, 1000);
   while (st.k < nch) {
-    trace(tr, 2, st.k);
+    trace(tr, 3, 60000 + st.k);
     deblock_chunk(a, r, L.db, st);
   }
-  trace(tr, 2, 100000);
+  trace(tr, 3, 100000);
 }
 
 // ---------------------------------------------------------------------------

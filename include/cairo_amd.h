@@ -176,6 +176,8 @@ typedef struct cairo_peer {
   uint64_t ring_addr, coef_addr, progress_addr; /* device addresses in the owner's process */
   uint8_t ipc[3][64];                           /* hipIpcMemHandle_t of the three buffers */
 } cairo_peer;
+/* (A member's exported output_cache, 2 bytes x 1.5 x Wa x Ha x stages, must
+ * stay below 2 GiB: larger IPC imports did not return on the test boxes.) */
 CAIRO_API int cairo_ctx_peer_info(cairo_ctx *ctx, int cross_device, cairo_peer *out);
 CAIRO_API int cairo_ctx_join_group(cairo_ctx *ctx, int size, int rank, const cairo_peer *peers);
 /* Launch the pending (partial) batch now. */
