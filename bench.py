@@ -392,6 +392,27 @@ def main():
         dist.destroy_process_group()
 
 
+def agreed_step(dist, group, rank, state, what, fn):
+    """Run fn unless a rank already failed, then agree on failure over
+    `group`: every rank makes the same collective call whatever happened, so
+    a rank that failed never leaves the others waiting in a barrier.  state
+    ["err"] holds this rank's first error; returns True while all ranks are
+    fine."""
+    import torch
+
+    if not state["err"]:
+        try:
+            fn()
+        except Exception as ex:  # noqa: BLE001 -- reported in the line
+            state["err"] = f"rank {rank} ({what}): {type(ex).__name__}: {ex}"[:300]
+            note(rank, f"failed: {state['err']}")
+    bad = torch.tensor([1.0 if state["err"] else 0.0], dtype=torch.float64)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=group)
+    if bad.item() and not state["err"]:
+        state["err"] = f"rank {rank}: stopped ({what}): another rank failed"
+    return not state["err"]
+
+
 def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, barrier, dist, dev, world, rank,
                   local, share):
     """N > 1: ONE stream over all ranks, frame-interleaved:
@@ -411,20 +432,7 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
     state = {"err": ""}
 
     def step(what, fn):
-        """Run fn unless a rank already failed, then agree on failure: every
-        rank makes the same collective calls whatever happened (a rank that
-        failed must not leave the others in a barrier)."""
-        if not state["err"]:
-            try:
-                fn()
-            except Exception as ex:  # noqa: BLE001 -- reported in the line
-                state["err"] = f"rank {rank} ({what}): {type(ex).__name__}: {ex}"[:300]
-                note(rank, f"single stream failed: {state['err']}")
-        bad = torch.tensor([1.0 if state["err"] else 0.0], dtype=torch.float64)
-        dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=gloo)
-        if bad.item() and not state["err"]:
-            state["err"] = f"rank {rank}: stopped ({what}): another rank failed"
-        return not state["err"]
+        return agreed_step(dist, gloo, rank, state, what, fn)
 
     def run(first, count, keep):
         inflight = deque()
