@@ -1935,7 +1935,10 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 // deadlock with every workgroup resident.
 // ---------------------------------------------------------------------------
 
-constexpr int kPrioFrameMBs = 4000;  // helpers get issue priority above this frame size
+#ifndef CAIRO_PRIO_FRAME_MBS
+#define CAIRO_PRIO_FRAME_MBS 4000
+#endif
+constexpr int kPrioFrameMBs = CAIRO_PRIO_FRAME_MBS;  // helpers get issue priority above this frame size
 
 // Pool of workgroup b out of n, nh of them helpers: spread evenly over the
 // block indices (so over every XCD, which take blocks round-robin), and a
