@@ -6,11 +6,11 @@ ring R = 4 (3 inter references), quality 16, band4 synthetic content
 (seed 1234).  --config 720p / 1080p run configs[1] / configs[2].
 
 A step = one engine launch's batch of P-frames (the library's default frames
-per launch for the frame size: 24 at 4K, 32 at 1080p and 720p) through the
+per launch for the frame size: 28 at 4K, 32 at 1080p and 720p) through the
 hot path: RGB->YUV, inter search, the macroblock wavefront (intra search,
 classify, transform, VAQ, quantize, reconstruct, in-loop deblock), the
 entropy precode, and each frame's block table + feed bits handed to host
-memory for the arithmetic coder.  --steps 20 therefore times 480 4K frames.  All input frames are
+memory for the arithmetic coder.  --steps 20 therefore times 560 4K frames.  All input frames are
 resident in HBM before the timed region.
 
 Other legs (rank 0, N = 1), outside the timed region:

@@ -48,11 +48,11 @@ constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engi
 // tools/batch_sweep.sh).  With the pools shared between consecutive launches
 // (k_engine next_task) a batch's tail no longer idles half the workers, so
 // larger batches pay: 32 up to about 1080p (1080p: 2981 at 12, 3460 at 24,
-// 3551 at 32 Mpix/s), 24 above (4K: 3868 at 20, 4021-4030 at 24, 4035 at 28,
-// 3974 at 32).
+// 3551 at 32 Mpix/s), 28 above (final engine, 4K: 4222 at 20, 4389-4413 at
+// 24, 4443-4454 at 28, 4235 at 32).
 constexpr int kMidFrameMBs = 16000;
 inline int default_batch(size_t mbs) {
-  return mbs <= (size_t)kMidFrameMBs ? 32 : 24;
+  return mbs <= (size_t)kMidFrameMBs ? 32 : 28;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)

@@ -100,7 +100,7 @@ CAIRO_API int cairo_ctx_sync(cairo_ctx *ctx);
 /* Staging slots = frames that may be in flight (submitted, not released). */
 CAIRO_API int cairo_ctx_stages(const cairo_ctx *ctx);
 /* Frames per engine launch, 1..min(32, stages/2) (default 32 for frames of up to
- * 16000 macroblocks, 24 above). */
+ * 16000 macroblocks, 28 above). */
 CAIRO_API int cairo_ctx_set_batch(cairo_ctx *ctx, int frames);
 /* The default frames per launch for a frame size (no device needed; 0 for an
  * empty size). */

@@ -1,7 +1,7 @@
 """GPU parity of the configurations bench.py times, and of the drop-in API.
 
 * The pipelined Context with the library's default frames per launch (32 at
-  720p and 1080p, 24 at 4K), several launches in flight on two streams sharing
+  720p and 1080p, 28 at 4K), several launches in flight on two streams sharing
   their worker pools and, above 4000 macroblocks, helper issue priority:
   exactly what bench.py's
   timed region runs (BASELINE.json configs[1..4]), frame by frame against the
@@ -44,10 +44,10 @@ def test_timed_1080p_default_batch(orc, cairo):
 
 
 def test_timed_4k_default_batch(orc, cairo):
-    """configs[3] on one GPU: 4K q=16 R=4, default 24 frames per launch with
-    helper priority, 27 frames: two overlapping launches, 3 live references."""
-    assert cairo.default_batch(3840, 2160) == 24
-    _run_batched(orc, cairo, 3840, 2160, 4, 16, 27, 0)
+    """configs[3] on one GPU: 4K q=16 R=4, default 28 frames per launch with
+    helper priority, 31 frames: two overlapping launches, 3 live references."""
+    assert cairo.default_batch(3840, 2160) == 28
+    _run_batched(orc, cairo, 3840, 2160, 4, 16, 31, 0)
 
 
 @pytest.mark.parametrize("q", [1, 8, 31])
