@@ -624,9 +624,14 @@ class Encoder:
         if rgb is None:
             raise ValueError("frame must be uint8 RGB888")
         _ck(self.L.evx_encoder_encode(self.h, _ptr(rgb), w, h, bs.h), "encode")
+        self._shape = (w, h)
 
     def peek(self, state: int, width: int, height: int) -> np.ndarray:
         """Debug view of the last encoded frame (EVX_PEEK_*, evx1.h) -> RGB (h, w, 3)."""
+        # the native peek writes the encoder's frame size: refuse a smaller view
+        if getattr(self, "_shape", None) != (width, height):
+            raise ValueError(f"peek size {width}x{height} differs from the last encoded frame "
+                             f"{getattr(self, '_shape', None)}")
         out = np.zeros((height, width, 3), np.uint8)
         _ck(self.L.evx_encoder_peek(self.h, state, _ptr(out)), "peek")
         return out
