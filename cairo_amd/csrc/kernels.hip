@@ -172,6 +172,15 @@ __device__ __forceinline__ void acquire_fence(bool sys) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
+// Poll back-off (s_sleep units of 64 clocks) of the progress-word waits and of
+// the granule re-polls; overridable at build time for sweeps.
+#ifndef CAIRO_WAIT_SLEEP
+#define CAIRO_WAIT_SLEEP 2
+#endif
+#ifndef CAIRO_GRAN_SLEEP
+#define CAIRO_GRAN_SLEEP 1
+#endif
+
 // Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
 // timeout (~2 s) the error word is set and the wait gives up, so every
 // workgroup still drains and the host reports EVX_ERROR_HARDWAREFAIL.
@@ -181,7 +190,7 @@ __device__ __forceinline__ void wait_at_least(int32_t* word, int target, int32_t
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -219,7 +228,7 @@ __device__ __forceinline__ uint32_t gran_settle(const uint64_t* p, uint64_t g, u
   if ((uint32_t)(g >> 32) == tag) return (uint32_t)g;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(CAIRO_GRAN_SLEEP);
     g = gran_ld(p);
     if ((uint32_t)(g >> 32) == tag) break;
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
