@@ -59,3 +59,16 @@ def test_default_batch(cairo):
     assert cairo.default_batch(1920, 1080) == 32
     assert cairo.default_batch(3840, 2160) == 28
     assert cairo.default_batch(0, 720) == 0
+
+
+def test_peek_refuses_other_size(cairo):
+    """peek() writes the encoder's frame size (evx1enc.cpp:170-305): the
+    wrapper refuses a view of any other size before the native call (no GPU)."""
+    import pytest
+
+    e = cairo.Encoder()
+    try:
+        with pytest.raises(ValueError):
+            e.peek(cairo.PEEK_SOURCE, 16, 16)
+    finally:
+        e.close()
