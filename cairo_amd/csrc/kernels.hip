@@ -1948,6 +1948,9 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 #define CAIRO_PRIO_FRAME_MBS 4000
 #endif
 constexpr int kPrioFrameMBs = CAIRO_PRIO_FRAME_MBS;  // helpers get issue priority above this frame size
+#ifndef CAIRO_PRIO_LEVEL
+#define CAIRO_PRIO_LEVEL 2
+#endif
 
 // Pool of workgroup b out of n, nh of them helpers: spread evenly over the
 // block indices (so over every XCD, which take blocks round-robin), and a
@@ -2022,7 +2025,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
     // The helpers' inter records gate every row coder at its group starts:
     // on large frames they win the SIMD issue arbitration against the coders'
     // waves (A/B: 1080p +3 %, 4K +3 %; 720p -1 %, so not there).
-    if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(2);
+    if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(CAIRO_PRIO_LEVEL);
     for (;;) {
       bool prev;
       const int t = next_task(e, SyncLayout::kTicketHelpers, total, L, prev);
