@@ -88,6 +88,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_set_batch": (I, [P, I]),
         "cairo_ctx_peer_info": (I, [P, I, P]),
         "cairo_ctx_join_group": (I, [P, I, I, P]),
+        "cairo_group_check_queues": (I, [I]),
         "cairo_ctx_flush": (I, [P]),
         "cairo_ctx_set_helpers": (I, [P, I]),
         "cairo_ctx_max_workgroups": (I, [P]),
@@ -96,6 +97,7 @@ def lib() -> ctypes.CDLL:
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "cairo_serialize_feed": (I, [P, ctypes.c_uint64, P, U, ctypes.POINTER(U)]),
+        "cairo_precode_slice": (I, [P, U, U, U, P, P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
         "cairo_ctx_set_outputs": (I, [P, I]),
         "cairo_ctx_fetch_coef": (I, [P, I, P]),
         "cairo_unserialize_slice": (I, [P, ctypes.POINTER(U), U, U, U, U, P, P, P, P]),
@@ -294,6 +296,12 @@ class Context:
     def sync(self) -> None:
         _ck(self.L.cairo_ctx_sync(self.h), "cairo_ctx_sync")
 
+    def reset(self) -> None:
+        """Fresh-encoder state (cairo_ctx_reset): planes zeroed, tickets from 0,
+        any group left (its members reset and rejoin together)."""
+        _ck(self.L.cairo_ctx_reset(self.h), "cairo_ctx_reset")
+        self._keep.clear()
+
     def read_planes(self, which: int):
         """which: 0 input, 1 output_cache, 2+k ring slot k -> (y, u, v)."""
         y = np.empty((self.ha, self.wa), np.int16)
@@ -408,10 +416,22 @@ class Group:
                 m.set_batch(batch)
             if per_dev[d] > 1:  # members on one device share its workgroup slots
                 m.set_workgroups(max(1, m.max_workgroups() // per_dev[d]))
-        recs = [m.peer_info(cross_device=cross) for m in self.members]
+        self.cross = cross
+        self._join()
+        self.size, self.ring, self.stages = n, ring, stages
+        self.tickets = {}
+
+    def _join(self) -> None:
+        recs = [m.peer_info(cross_device=self.cross) for m in self.members]
         for r, m in enumerate(self.members):
             m.join_group(r, recs)
-        self.size, self.ring, self.stages = n, ring, stages
+
+    def reset(self) -> None:
+        """Every member back to the fresh-encoder state and the group rejoined
+        (cairo_ctx_reset leaves it): the next frame is frame 0 of a new stream."""
+        for m in self.members:
+            m.reset()
+        self._join()
         self.tickets = {}
 
     def submit(self, rgb, index: int, inter: bool, quality: int, on_device: bool = False) -> None:
@@ -475,6 +495,20 @@ def serialize_feed(feed: np.ndarray, feed_bits: int, capacity_bytes: int | None 
     f = np.ascontiguousarray(feed, dtype=np.uint32)
     _ck(lib().cairo_serialize_feed(_ptr(f), feed_bits, _ptr(out), cap, ctypes.byref(pos)), "cairo_serialize_feed")
     return out[: (pos.value + 7) // 8].tobytes(), pos.value
+
+
+def precode_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv):
+    """The host precode alone -> (feed words uint32, feed bits): what the GPU
+    precode hands over for a FEED_VALID frame."""
+    t = np.ascontiguousarray(table).view(np.uint8)
+    cy, cu, cv = (np.ascontiguousarray(a, dtype=np.int16) for a in (cy, cu, cv))
+    nb = ctypes.c_uint64(0)
+    L = lib()
+    L.cairo_precode_slice(_ptr(t), wmb, hmb, ring, _ptr(cy), _ptr(cu), _ptr(cv), None, 0, ctypes.byref(nb))
+    out = np.zeros((nb.value + 31) // 32 + 1, np.uint32)
+    _ck(L.cairo_precode_slice(_ptr(t), wmb, hmb, ring, _ptr(cy), _ptr(cu), _ptr(cv), _ptr(out), out.size,
+                              ctypes.byref(nb)), "cairo_precode_slice")
+    return out[: (nb.value + 31) // 32], nb.value
 
 
 def unserialize_slice(payload: bytes, nbits: int, wmb: int, hmb: int, ring: int, table=None, planes=None,

@@ -156,6 +156,11 @@ struct cairo_ctx {
   FrameArgs* fdesc_host = nullptr;  // pinned [kLaunchSlots][kMaxBatch]: per-frame views per launch
   FrameArgs* fdesc = nullptr;       // device copy
   int fdesc_next = 0;
+  // the H2D copy of each fdesc_host slot: a slot is rewritten only after its
+  // previous copy ran (more than kLaunchSlots launches may be queued, e.g.
+  // batch 1 with 96 staging slots, and the copy waits behind earlier launches)
+  hipEvent_t fdesc_done[kLaunchSlots] = {};
+  bool fdesc_used[kLaunchSlots] = {};
   int32_t* trace_host = nullptr;  // diagnostic live trace (mapped), opt-in via set_debug(4)
   int32_t* trace_dev = nullptr;
   size_t sync_words = 0;
@@ -290,6 +295,8 @@ void free_ctx(cairo_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->batch_ready)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->fdesc_done)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
   if (c->feed_host) (void)hipHostFree(c->feed_host);
   if (c->fs) (void)hipStreamDestroy(c->fs);
@@ -332,7 +339,14 @@ int zero_state(cairo_ctx* c) {
   c->batches = 0;
   c->prev_total = 0;  // its sync areas are zero now
   c->fresh = true;  // the first frame after a reset depends on no earlier frame
-  for (auto& s : c->st) *s.err = 0;
+  // tickets restart at 0 (every stage is idle here): a group member's k-th
+  // frame after a (re)join is its ticket k, which its peers assume when they
+  // locate its output_cache and progress words (frame_links)
+  c->next_ticket = 0;
+  for (auto& s : c->st) {
+    *s.err = 0;
+    s.ticket = -1;
+  }
   return kSuccess;
 }
 
@@ -364,6 +378,7 @@ int flush(cairo_ctx* c) {
   // launch may still be pending when this one is written)
   const int fslot = c->fdesc_next;
   c->fdesc_next = (c->fdesc_next + 1) % kLaunchSlots;
+  if (c->fdesc_used[fslot]) CK(hipEventSynchronize(c->fdesc_done[fslot]));
   FrameArgs* fh = c->fdesc_host + (size_t)fslot * kMaxBatch;
   FrameArgs* fd = c->fdesc + (size_t)fslot * kMaxBatch;
   bool any_inter = false;
@@ -422,6 +437,8 @@ int flush(cairo_ctx* c) {
     }
   }
   CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, st));
+  CK(hipEventRecord(c->fdesc_done[fslot], st));
+  c->fdesc_used[fslot] = true;
   CK(hipMemsetAsync(e.sync, 0, c->sync_words * sizeof(int32_t), st));
   if (c->stamps) {  // engine entry (min) / exit (max) words
     static const uint64_t init[2] = {~0ull, 0};
@@ -647,6 +664,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipEventCreate(&c->t_base));
   for (auto& ev : c->batch_end) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : c->batch_ready) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (auto& ev : c->fdesc_done) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 #undef TRY
   r = zero_state(c);
   if (r != kSuccess) {
@@ -940,14 +958,24 @@ int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
   if (r) return r;
   for (const Stage& s : c->st)
     if (s.busy) return kInvalidResource;
-  if ((outputs & CAIRO_OUT_FEED) && !c->feed_dev) {
+  if ((outputs & CAIRO_OUT_FEED) && !c->feed_host) {
+    // all or nothing: a partial allocation would leave feed_dev set with no
+    // host buffer for the precode to write into
     const size_t S = (size_t)c->stages;
-    c->feed_words = feed_words_per_slot(c->mbs);
-    CK(hipMalloc(&c->feed_dev, c->feed_words * 4 * S));
-    CK(hipMalloc(&c->feed_hdr, kFeedHdrWords * 4 * S));
-    CK(hipMalloc(&c->feed_scratch, kFeedScratchPerMB * c->mbs * 4 * S));
-    CK(hipHostMalloc(&c->feed_host, (kFeedHdrWords + c->feed_words) * 4 * S, hipHostMallocMapped));
-    if (c->ps_own) {  // (the A/B variant: each stream takes a hardware queue)
+    const size_t words = feed_words_per_slot(c->mbs);
+    uint32_t *dev = nullptr, *hdr = nullptr, *scratch = nullptr, *host = nullptr;
+    hipError_t e = hipMalloc(&dev, words * 4 * S);
+    if (e == hipSuccess) e = hipMalloc(&hdr, kFeedHdrWords * 4 * S);
+    if (e == hipSuccess) e = hipMalloc(&scratch, kFeedScratchPerMB * c->mbs * 4 * S);
+    if (e == hipSuccess) e = hipHostMalloc(&host, (kFeedHdrWords + words) * 4 * S, hipHostMallocMapped);
+    if (e != hipSuccess) {
+      for (void* q : {(void*)dev, (void*)hdr, (void*)scratch}) (void)hipFree(q);
+      if (host) (void)hipHostFree(host);
+      return fail(e, "set_outputs: feed buffers");
+    }
+    c->feed_words = words;
+    c->feed_dev = dev, c->feed_hdr = hdr, c->feed_scratch = scratch, c->feed_host = host;
+    if (c->ps_own && !c->ps) {  // (the A/B variant: each stream takes a hardware queue)
       CK(hipStreamCreateWithFlags(&c->ps, hipStreamNonBlocking));
       for (auto& ev : c->pre_done) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
@@ -1044,6 +1072,27 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
   return kSuccess;
 }
 
+int cairo_group_check_queues(int local_members) {
+  // Members in one process on one device share that process's hardware
+  // queues (GPU_MAX_HW_QUEUES, HIP's default 4).  Each member keeps two launch
+  // streams and a copy stream busy; when two members' persistent launches
+  // land in one in-order queue, the later cannot start until the earlier
+  // ends, which waits on it: a deadlock the bounded in-kernel waits would
+  // only report as EVX_ERROR_HARDWAREFAIL after 2 s.  Refuse up front.
+  if (local_members < 2) return kSuccess;
+  const char* env = getenv("GPU_MAX_HW_QUEUES");
+  const int have = env && *env ? atoi(env) : 4;
+  const int need = 3 * local_members + 2;
+  if (need > 32 || have < need) {
+    fprintf(stderr,
+            "[cairo_amd] join_group: %d members share this process and device; they need GPU_MAX_HW_QUEUES >= %d "
+            "(have %d, at most 32); run one process per member, or set GPU_MAX_HW_QUEUES before the first HIP call\n",
+            local_members, need, have);
+    return kInvalidArg;
+  }
+  return kSuccess;
+}
+
 int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* peers) {
   if (!c || !peers || size < 1 || size > kMaxGroup || rank < 0 || rank >= size) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1052,9 +1101,11 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
   if (size == 1) return kSuccess;
   const pid_t me = getpid();
   bool sys = false;
+  int local = 0;  // members in this process on this device, this one included
   for (int i = 0; i < size; i++) {
     const cairo_peer& p = peers[i];
     if (p.width != c->w || p.height != c->h || p.ring != c->ring || p.stages < 2) return kInvalidArg;
+    if (i == rank || (p.pid == me && p.device == c->device)) local++;
     if (i == rank) continue;
     if (p.pid != me || p.device != c->device) sys = true;
     if (p.device != c->device || p.pid != me) {
@@ -1064,6 +1115,7 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
       }
     }
   }
+  if (cairo_group_check_queues(local) != kSuccess) return kInvalidArg;
   for (int i = 0; i < size; i++) {
     cairo_ctx::Peer& q = c->gp[i];
     const cairo_peer& p = peers[i];

@@ -313,10 +313,13 @@ int serialize_feed(const uint32_t* feed, uint64_t feed_bits, uint8_t* out, uint6
   // has slack) are never coded
   thread_local std::vector<uint64_t> words;
   const size_t n64 = (size_t)((feed_bits + 63) / 64);
+  const uint64_t n32 = (feed_bits + 31) / 32;
   const uint64_t* w = reinterpret_cast<const uint64_t*>(feed);
-  if ((uintptr_t)feed & 7) {  // unaligned: copy
+  // unaligned, or an odd count of 32-bit words (the last 64-bit read would
+  // pass the caller's buffer by 4 bytes): copy
+  if (((uintptr_t)feed & 7) || (n32 & 1)) {
     words.assign(n64, 0);
-    memcpy(words.data(), feed, (size_t)((feed_bits + 31) / 32) * 4);
+    memcpy(words.data(), feed, (size_t)n32 * 4);
     w = words.data();
   }
   return code_feed(w, feed_bits, out, out_bits_capacity, bit_pos);
@@ -334,12 +337,9 @@ int serialize_result(cairo_ctx* ctx, int ticket, cairo_frame_result* res, uint32
                          out_bits_capacity, bit_pos);
 }
 
-int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t ring,
-                    const int16_t* cy, const int16_t* cu, const int16_t* cv, uint8_t* out,
-                    uint64_t out_bits_capacity, uint64_t* bit_pos) {
-  const uint64_t pos0 = *bit_pos;
-  if (pos0 > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
-  thread_local std::vector<uint64_t> feed_words;
+// The precode of a slice into `words` (LSB-first feed); returns its bit count.
+uint64_t precode_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t ring, const int16_t* cy,
+                       const int16_t* cu, const int16_t* cv, std::vector<uint64_t>& feed_words) {
   feed_words.clear();
   Feed f{&feed_words};
   const uint32_t count = (uint16_t)(wmb * hmb);  // uint16 block_count, serialize.cpp:321
@@ -399,7 +399,16 @@ int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t r
   plane_blocks(f, cv, wa / 2, ha / 2, 8, table);
 
   f.close();
-  return code_feed(feed_words.data(), f.nbits, out, out_bits_capacity, bit_pos);
+  return f.nbits;
+}
+
+int serialize_slice(const uint8_t* table, uint32_t wmb, uint32_t hmb, uint32_t ring,
+                    const int16_t* cy, const int16_t* cu, const int16_t* cv, uint8_t* out,
+                    uint64_t out_bits_capacity, uint64_t* bit_pos) {
+  if (*bit_pos > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT
+  thread_local std::vector<uint64_t> feed_words;
+  const uint64_t nbits = precode_slice(table, wmb, hmb, ring, cy, cu, cv, feed_words);
+  return code_feed(feed_words.data(), nbits, out, out_bits_capacity, bit_pos);
 }
 
 }  // namespace cairo
@@ -411,6 +420,19 @@ extern "C" int cairo_serialize_feed(const uint32_t* feed, uint64_t feed_bits, ui
   int r = cairo::serialize_feed(feed, feed_bits, out, (uint64_t)out_bytes * 8u, &pos);
   *bit_pos = (uint32_t)pos;
   return r;
+}
+
+extern "C" int cairo_precode_slice(const uint8_t* block_table, uint32_t wmb, uint32_t hmb, uint32_t ring,
+                                   const int16_t* cy, const int16_t* cu, const int16_t* cv, uint32_t* feed,
+                                   uint64_t feed_words, uint64_t* feed_bits) {
+  if (!block_table || !cy || !cu || !cv || !feed_bits) return 1;
+  std::vector<uint64_t> words;
+  const uint64_t nbits = cairo::precode_slice(block_table, wmb, hmb, ring, cy, cu, cv, words);
+  *feed_bits = nbits;
+  const uint64_t need = (nbits + 31) / 32;
+  if (!feed || feed_words < need) return 7;  // EVX_ERROR_CAPACITY_LIMIT: *feed_bits says how much is needed
+  memcpy(feed, words.data(), (size_t)need * 4);
+  return 0;
 }
 
 extern "C" int cairo_serialize_slice(const uint8_t* block_table, uint32_t wmb, uint32_t hmb,

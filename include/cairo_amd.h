@@ -180,6 +180,13 @@ typedef struct cairo_peer {
  * stay below 2 GiB: larger IPC imports did not return on the test boxes.) */
 CAIRO_API int cairo_ctx_peer_info(cairo_ctx *ctx, int cross_device, cairo_peer *out);
 CAIRO_API int cairo_ctx_join_group(cairo_ctx *ctx, int size, int rank, const cairo_peer *peers);
+/* Whether local_members group members may share one process and device:
+ * they need GPU_MAX_HW_QUEUES >= 3 * local_members + 2 (at most 32), or two
+ * members' persistent launches can land in one in-order hardware queue and
+ * deadlock.  0 = fine (always for fewer than 2), else EVX_ERROR_INVALID_ARGS
+ * with a message on stderr.  cairo_ctx_join_group applies it; no device
+ * needed. */
+CAIRO_API int cairo_group_check_queues(int local_members);
 /* Launch the pending (partial) batch now. */
 CAIRO_API int cairo_ctx_flush(cairo_ctx *ctx);
 /* Choose the outputs (CAIRO_OUT_COEF and/or CAIRO_OUT_FEED) for frames
@@ -213,6 +220,14 @@ CAIRO_API int cairo_serialize_slice(const uint8_t *block_table, uint32_t wmb, ui
  * with CAIRO_FEED_VALID): only the arithmetic coder runs. */
 CAIRO_API int cairo_serialize_feed(const uint32_t *feed, uint64_t feed_bits, uint8_t *out,
                                    uint32_t out_bytes, uint32_t *bit_pos);
+/* The host precode alone (serialize.cpp:10-286, stream.cpp:550-581,
+ * golomb.cpp:8-91, with the 32 Mbit per-section drop rule): the feed bits the
+ * arithmetic coder consumes, LSB-first in 32-bit words -- what the GPU precode
+ * writes for a CAIRO_FEED_VALID frame.  *feed_bits receives the bit count;
+ * EVX_ERROR_CAPACITY_LIMIT (7) if feed_words cannot hold them. */
+CAIRO_API int cairo_precode_slice(const uint8_t *block_table, uint32_t wmb, uint32_t hmb, uint32_t ring,
+                                  const int16_t *coef_y, const int16_t *coef_u, const int16_t *coef_v,
+                                  uint32_t *feed, uint64_t feed_words, uint64_t *feed_bits);
 
 /* ---- host entropy decode (unserialize_slice, unserialize.cpp:321-342) ----
  * Decodes the ABAC payload of one frame starting at bit *read_index of data

@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--frames", type=int, default=12)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--intra-every", type=int, default=0)
+    ap.add_argument("--rejoin", type=int, default=0, help="inproc: reset, rejoin and encode the stream again, N times")
     ap.add_argument("--feed", action="store_true", help="members hand over GPU-precoded feeds (bench's mode); "
                                                          "payloads are checked too")
     a = ap.parse_args()
@@ -81,17 +82,20 @@ def main():
     if a.mode == "inproc":
         g = cairo_amd.Group(w, h, ring, [0] * N, batch=a.batch)
         assert F <= N * g.stages  # every frame in flight at once
-        for t in range(F):
-            g.submit(orc.make_frame(w, h, t), t, not ref[t][0], q)
-        for t in range(F):
-            out = g.wait(t)
-            if table_mismatch(out.table, ref[t][1]) or any(
-                    not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
-                bad.append(t)
-            g.release(t)
-        for t, planes in final.items():
-            if any(not np.array_equal(x, y) for x, y in zip(g.recon(t), planes)):
-                bad.append(f"recon {t}")
+        for rnd in range(1 + a.rejoin):
+            if rnd:  # reset every member and rejoin: a new stream from frame 0
+                g.reset()
+            for t in range(F):
+                g.submit(orc.make_frame(w, h, t), t, not ref[t][0], q)
+            for t in range(F):
+                out = g.wait(t)
+                if table_mismatch(out.table, ref[t][1]) or any(
+                        not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
+                    bad.append(f"{t}" + (f" (after rejoin {rnd})" if rnd else ""))
+                g.release(t)
+            for t, planes in final.items():
+                if any(not np.array_equal(x, y) for x, y in zip(g.recon(t), planes)):
+                    bad.append(f"recon {t}" + (f" (after rejoin {rnd})" if rnd else ""))
         g.close()
     else:
         import torch.distributed as dist

@@ -72,3 +72,19 @@ def test_peek_refuses_other_size(cairo):
             e.peek(cairo.PEEK_SOURCE, 16, 16)
     finally:
         e.close()
+
+
+def test_group_queue_check(cairo, monkeypatch):
+    """In-process group members on one device need GPU_MAX_HW_QUEUES >= 3N+2
+    (backend.hip cairo_group_check_queues; cairo_ctx_join_group applies it):
+    refused with a diagnosis instead of a 2 s in-kernel timeout.  No GPU."""
+    L = cairo.lib()
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    assert L.cairo_group_check_queues(1) == 0  # one member per process: the production layout
+    assert L.cairo_group_check_queues(2) == 1  # HIP's default 4 < 8
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    assert L.cairo_group_check_queues(2) == 0
+    assert L.cairo_group_check_queues(3) == 1
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "32")
+    assert L.cairo_group_check_queues(10) == 0
+    assert L.cairo_group_check_queues(11) == 1  # 35 queues: more than HIP allows

@@ -37,6 +37,25 @@ def test_group_in_process(members, ring, w, h, frames, intra):
     assert json.loads(r.stdout.strip().splitlines()[-1])["mismatched"] == []
 
 
+def test_group_reset_rejoin():
+    """Members reset (cairo_ctx_reset: tickets restart at 0) and rejoin, then
+    encode the stream again from frame 0: their peers locate each member's
+    output_cache and progress words by ticket, so both passes are bit-exact."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
+    r = _run(["inproc", "--members", 2, "--ring", 4, "--frames", 10, "--batch", 3, "--rejoin", 1], env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["mismatched"] == []
+
+
+def test_group_in_process_refuses_few_queues():
+    """Two in-process members under HIP's default 4 hardware queues would
+    deadlock; join_group refuses with a diagnosis instead."""
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    r = _run(["inproc", "--members", 2, "--ring", 4, "--frames", 4, "--batch", 2], env=env)
+    assert r.returncode != 0
+    assert "GPU_MAX_HW_QUEUES" in r.stderr
+
+
 def test_group_4k_in_process():
     """BASELINE configs[3] geometry, two members, default launches."""
     env = dict(os.environ, GPU_MAX_HW_QUEUES="8")

@@ -228,11 +228,27 @@ def test_encoder_stream_matches_golden(orc, cairo, cfg):
 # the GPU with row-level dependencies); every frame must still match.
 # ---------------------------------------------------------------------------
 
-def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None, workgroups=0):
+def _payload_bits(cairo, out, ctx, ring, tk):
+    """A frame's ABAC payload (after the header and frame descriptor) from its
+    outputs, as a bit array: from the GPU precode's feed when valid, else from
+    the planes (fetched for a feed-only context)."""
+    if out.feed_status == cairo.FEED_VALID:
+        data, n = cairo.serialize_feed(out.feed, out.feed_bits)
+    else:
+        cy, cu, cv = (out.coef_y, out.coef_u, out.coef_v) if out.coef_y is not None else ctx.fetch_coef(tk)
+        data, n = cairo.serialize_slice(out.table, ctx.wmb, ctx.hmb, ring, cy, cu, cv)
+    return np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[:n]
+
+
+def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None, workgroups=0, outputs=0):
     """Frames through one pipelined Context (up to `stages` in flight, `batch`
     frames per launch, 0 = the library default; consecutive launches overlap
     on two streams) vs the oracle: block table and coefficients of every
-    frame, then every ring slot at the end."""
+    frame, then every ring slot at the end.  outputs = the context's
+    set_outputs (0: the default, coefficient planes); with OUT_FEED, as
+    bench.py times it, every frame's payload bits (coded from the GPU
+    precode's feed) are compared with the oracle's stream record too, and
+    the coefficients are fetched from the staging slot."""
     gen = gen or orc.make_frame
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
@@ -242,10 +258,14 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
         intra = t == 0 or (intra_every and t % intra_every == 0)
         if intra:
             e.insert_intra()
-        e.encode(rgb)
-        ref.append((intra, e.block_table(), e.planes(1)))
+        data, nbits = e.encode(rgb)
+        head = (14 * 8 if t == 0 else 0) + 10 * 8  # header + frame descriptor precede the payload
+        bits = np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[head:nbits]
+        ref.append((intra, e.block_table(), e.planes(1), bits))
     final_slots = [e.planes(2 + k) for k in range(ring)]
     ctx = cairo.Context(w, h, ring)
+    if outputs:
+        ctx.set_outputs(outputs)
     if batch:
         ctx.set_batch(batch)
     if workgroups:
@@ -257,9 +277,15 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
         out = ctx.wait(tk)
         tag = f"{w}x{h} R={ring} q={q} batch={batch} frame {t}"
         _table_equal(out.table, ref[t][1], f"{tag}: block table")
-        np.testing.assert_array_equal(out.coef_y, ref[t][2][0], err_msg=f"{tag}: coef Y")
-        np.testing.assert_array_equal(out.coef_u, ref[t][2][1], err_msg=f"{tag}: coef U")
-        np.testing.assert_array_equal(out.coef_v, ref[t][2][2], err_msg=f"{tag}: coef V")
+        coef = (out.coef_y, out.coef_u, out.coef_v) if out.coef_y is not None else ctx.fetch_coef(tk)
+        np.testing.assert_array_equal(coef[0], ref[t][2][0], err_msg=f"{tag}: coef Y")
+        np.testing.assert_array_equal(coef[1], ref[t][2][1], err_msg=f"{tag}: coef U")
+        np.testing.assert_array_equal(coef[2], ref[t][2][2], err_msg=f"{tag}: coef V")
+        if outputs & cairo.OUT_FEED:
+            assert out.feed_status == cairo.FEED_VALID, f"{tag}: feed status {out.feed_status}"
+            got = _payload_bits(cairo, out, ctx, ring, tk)
+            assert got.size == ref[t][3].size, f"{tag}: payload {got.size} vs {ref[t][3].size} bits"
+            assert np.array_equal(got, ref[t][3]), f"{tag}: payload bits differ"
         ctx.release(tk)
 
     for t in range(frames):  # at most `stages` frames in flight (submitted, not released)

@@ -31,29 +31,40 @@ API_BIN = os.path.join(ROOT, "cairo_amd", "_lib", "evx1_api_caller")
 
 def test_timed_720p_default_batch(orc, cairo):
     """configs[1]: 720p q=16 R=2, default 32 frames per launch, 40 frames = a
-    full launch + a partial one overlapping it."""
+    full launch + a partial one overlapping it; feed outputs as bench.py
+    times them, every frame's payload bits against the oracle's record."""
     assert cairo.default_batch(1280, 720) == 32
-    _run_batched(orc, cairo, 1280, 720, 2, 16, 40, 0)
+    _run_batched(orc, cairo, 1280, 720, 2, 16, 40, 0, outputs=cairo.OUT_FEED)
 
 
 def test_timed_1080p_default_batch(orc, cairo):
     """configs[2]: 1080p q=8 R=4 (8 zero rows of padding), default 32 frames
-    per launch, 36 frames: all three references live, two overlapping launches."""
+    per launch, 36 frames: all three references live, two overlapping
+    launches; feed outputs, payloads checked."""
     assert cairo.default_batch(1920, 1080) == 32
-    _run_batched(orc, cairo, 1920, 1080, 4, 8, 36, 0)
+    _run_batched(orc, cairo, 1920, 1080, 4, 8, 36, 0, outputs=cairo.OUT_FEED)
 
 
 def test_timed_4k_default_batch(orc, cairo):
     """configs[3] on one GPU: 4K q=16 R=4, default 28 frames per launch with
-    helper priority, 31 frames: two overlapping launches, 3 live references."""
+    helper priority, 31 frames: two overlapping launches, 3 live references;
+    feed outputs (bench.py's timed mode), payloads checked."""
     assert cairo.default_batch(3840, 2160) == 28
-    _run_batched(orc, cairo, 3840, 2160, 4, 16, 31, 0)
+    _run_batched(orc, cairo, 3840, 2160, 4, 16, 31, 0, outputs=cairo.OUT_FEED)
 
 
-@pytest.mark.parametrize("q", [1, 8, 31])
-def test_4k_quality_sweep(orc, cairo, q):
-    """configs[4]: the 4K quality sweep (VAQ on), default launch."""
-    _run_batched(orc, cairo, 3840, 2160, 4, q, 3, 0)
+def test_timed_4k_both_outputs(orc, cairo):
+    """The same launches with both outputs (coefficient planes D2H and the
+    feed): 4K, 6 frames."""
+    _run_batched(orc, cairo, 3840, 2160, 4, 16, 6, 0, outputs=cairo.OUT_FEED | cairo.OUT_COEF)
+
+
+@pytest.mark.parametrize("q,frames", [(1, 31), (8, 3), (31, 31)])
+def test_4k_quality_sweep(orc, cairo, q, frames):
+    """configs[4]: the 4K quality sweep (VAQ on), default launch, feed
+    outputs.  q = 1 and 31 (the ends of the sweep) over 31 frames: two
+    overlapping 28-frame launches, every payload against the oracle."""
+    _run_batched(orc, cairo, 3840, 2160, 4, q, frames, 0, outputs=cairo.OUT_FEED)
 
 
 @pytest.mark.parametrize("rows", [1, 3])
@@ -252,3 +263,36 @@ def test_submit_rejects_host_pointer_as_device(cairo):
     out = ctx.encode_frame(rgb, 0, False, 16)  # the context is still usable
     assert out.table.size == ctx.wmb * ctx.hmb
     ctx.close()
+
+
+def test_many_launches_queued(orc, cairo):
+    """More launches queued than the context keeps frame-view slots for (64):
+    96 staging slots, one frame per launch, 80 device frames submitted before
+    the first wait.  Each view slot is rewritten only after its earlier copy
+    to the device ran (backend.hip fdesc_done), so every frame is encoded from
+    its own views."""
+    import ctypes
+
+    w, h, ring, q, n = 64, 48, 2, 16, 80
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime the library uses
+    frames = np.stack([orc.make_frame(w, h, t) for t in range(n)])
+    dev = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(frames.nbytes)) == 0
+    try:
+        assert hip.hipMemcpy(dev, frames.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(frames.nbytes), 1) == 0
+        ctx = cairo.Context(w, h, ring)
+        assert ctx.stages == 96
+        ctx.set_batch(1)
+        fsz = w * h * 3
+        tks = [ctx.submit(dev.value + t * fsz, t, t > 0, q, on_device=True) for t in range(n)]
+        e = orc.OracleEncoder(ring)
+        e.set_quality(q)
+        for t, tk in enumerate(tks):
+            e.encode(frames[t])
+            out = ctx.wait(tk)
+            _table_equal(out.table, e.block_table(), f"frame {t}")
+            np.testing.assert_array_equal(out.coef_y, e.planes(1)[0], err_msg=f"frame {t}")
+            ctx.release(tk)
+        ctx.close()
+    finally:
+        hip.hipFree(dev)
