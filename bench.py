@@ -85,6 +85,10 @@ def parse():
     p.add_argument("--helpers", type=int, default=0, help="helper workgroups of a launch's workers (0 = default)")
     p.add_argument("--rows", type=int, default=0, help="row-coder (= helper) workgroups per launch (0 = library default)")
     p.add_argument("--stages", type=int, default=0, help="staging slots of the timed context (0 = library default)")
+    p.add_argument("--intervals", default=None,
+                   help="write the timed engine launches' [start, end) intervals (CSV, ms) to this path")
+    p.add_argument("--no-host-rgb", action="store_true", help="skip the pipelined host-RGB (PCIe-inclusive) leg")
+    p.add_argument("--host-rgb-steps", type=int, default=4, help="timed steps of the host-RGB leg")
     return p.parse_args()
 
 
@@ -263,7 +267,11 @@ def main():
 
     # the frames the bit-exact check compares (rank 0, N = 1: the oracle's sample)
     check = rank == 0 and world == 1 and not a.no_cpu_baseline
-    n_check = (a.cpu_frames or max(2, min(48, int(60e6 / (w * h))))) + 1 if check else 0
+    # CPU baseline: frame 0 + a bounded sample of P-frames (about 60 Mpixels)
+    cpu_pframes = a.cpu_frames or max(2, min(48, int(60e6 / (w * h))))
+    # bit-exact sample: every frame of the first launch and the head of the
+    # second (which overlaps the first and shares its workers), at least 31
+    n_check = max(cpu_pframes + 1, batch + 3, 31) if check else 0
     n_check = min(n_check, warm_frames)
     hot_records = {}
 
@@ -283,8 +291,16 @@ def main():
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    intervals = ctx.busy_intervals()
     kernel_ms, kframes = ctx.take_timings()
     launches = max(1, a.steps)
+    if a.intervals and rank == 0:
+        with open(a.intervals, "w") as fh:
+            fh.write(f"# {w}x{h} R={ring} q={q}: timed k_engine launches, {batch} frames each, {timed_frames} frames; "
+                     f"[start, end) ms on one HIP-event clock (launch streams)\n")
+            fh.write("launch,start_ms,end_ms,frames\n")
+            for i, (s0, s1) in enumerate(intervals):
+                fh.write(f"{i},{s0:.4f},{s1:.4f},{batch}\n")
     ctx.set_profiling(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
     value = aggregate_mpix(w, h, timed_frames, world, elapsed)
@@ -300,6 +316,7 @@ def main():
         "algorithmic_bytes": abytes["engine"], "per": "frame",
         "engine_busy_ms_per_frame": round(engine_busy_ms, 4),
         "avg_launch_ms": round(kernel_ms[2] / launches, 3), "frames_per_launch": batch,
+        "launches": int(len(intervals)),
         "note": "achieved = SURVEY §8(d) algorithmic bytes per frame / (engine busy time / frames); busy time = "
                 "union of the k_engine launch intervals (HIP events on the launch streams; two launches overlap, "
                 "avg_launch_ms is the per-launch duration rocprofv3 --stats reports)",
@@ -342,6 +359,10 @@ def main():
                          dev, world, n_check, e2e_records)
         ctx2.close()
     ctx.close()
+    host_leg = None
+    if not a.no_host_rgb and world == 1:
+        note(rank, "host-RGB leg")
+        host_leg = host_rgb(cairo_amd, a, w, h, ring, q, batch, local)
     single = None
     if world > 1 and not a.no_single_stream:
         note(rank, "single-stream leg")
@@ -377,13 +398,14 @@ def main():
         "roofline": roof,
         "roofline_valu": valu,
         "end_to_end": e2e,
+        "host_rgb": host_leg,
         "api_encode": api,
         "single_stream": single,
     }
     if check:
         note(rank, "CPU baseline and bit-exact check")
-        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, n_check - 1,
-                                                                   hot_records, e2e_records)
+        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, cpu_pframes, n_check - 1,
+                                                                   hot_records, e2e_records, batch)
     else:
         result["cpu_baseline"] = None
     if rank == 0:
@@ -569,6 +591,56 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier
             "note": "hot path + host entropy (native frame pipeline, cairo_stream_*); payload bits produced"}
 
 
+def host_rgb(cairo_amd, a, w, h, ring, q, batch, local):
+    """The hot path fed from host memory (PCIe-inclusive): frames in pinned
+    host buffers, each uploaded by the context inside the timed region
+    (cairo_ctx_submit with rgb_on_device = 0), feed outputs as in the timed
+    leg.  Not the headline value (that has the frames resident in HBM)."""
+    import torch
+
+    steps = max(1, a.host_rgb_steps)
+    warm, timed = batch, steps * batch
+    n = warm + timed
+    try:
+        pinned = torch.empty((n, h, w, 3), dtype=torch.uint8, pin_memory=True)
+    except RuntimeError as ex:  # pinned memory refused: report, do not fail the line
+        return {"error": f"pinned host frames: {ex}"[:200]}
+    host = pinned.numpy()
+    with ThreadPoolExecutor(max(1, min(8, host_cpus()))) as pool:
+        list(pool.map(lambda f: host.__setitem__(f, cairo_amd.make_band4(w, h, f)), range(n)))
+    ctx = cairo_amd.Context(w, h, ring, device=local)
+    ctx.set_batch(batch)
+    ctx.set_outputs(cairo_amd.OUT_FEED)
+    stages = ctx.stages
+
+    def run(first, count):
+        inflight = deque()
+        for f in range(first, first + count):
+            if len(inflight) == stages:
+                ff, t = inflight.popleft()
+                ctx.wait(t, copy=False)
+                ctx.release(t)
+            inflight.append((f, ctx.submit(host[f], f, f > 0, q, on_device=False)))
+        while inflight:
+            ff, t = inflight.popleft()
+            ctx.wait(t, copy=False)
+            ctx.release(t)
+
+    run(0, warm)
+    ctx.sync()
+    t0 = time.perf_counter()
+    run(warm, timed)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    ctx.close()
+    del host, pinned
+    return {"value": round(w * h * timed / el / 1e6, 3), "unit": "Mpix/s", "ms_per_frame": round(el * 1e3 / timed, 4),
+            "timed_frames": timed, "pcie_bytes_per_frame": 3 * w * h,
+            "pcie_GBps": round(3 * w * h * timed / el / 1e9, 2),
+            "note": "frames in pinned host memory, uploaded per launch inside the timed region (rgb_on_device=0); "
+                    "feed outputs; PCIe-inclusive rate, not the headline value"}
+
+
 def api_encode(w, h, ring, q, frames):
     """evx1_encoder::encode() timed by a C++ caller built against
     include/evx1.h (cairo_amd/_lib/evx1_api_caller): one synchronous call per
@@ -590,12 +662,13 @@ def api_encode(w, h, ring, q, frames):
                     "host entropy on the calling thread)"}
 
 
-def cpu_baseline(cairo_amd, w, h, ring, q, pframes, hot_records, e2e_records):
+def cpu_baseline(cairo_amd, w, h, ring, q, pframes, last, hot_records, e2e_records, batch):
     """The oracle (plain-C restatement of the reference encoder, test
-    infrastructure) on one host core over a bounded sample: frame 0 (I) +
-    `pframes` P-frames; P-frame Mpix/s.  The GPU records of the same frames,
-    taken from the timed hot-path context and from the end-to-end pipeline,
-    are then compared bit for bit (the checker role)."""
+    infrastructure) on one host core: frame 0 (I) + `pframes` P-frames timed
+    (a bounded sample); P-frame Mpix/s.  It then continues, untimed, to frame
+    `last`, and the GPU records of frames 0..last, taken from the timed
+    hot-path context and from the end-to-end pipeline, are compared bit for
+    bit (the checker role)."""
     from oracle import oracle as orc
 
     e = orc.OracleEncoder(ring)
@@ -603,29 +676,29 @@ def cpu_baseline(cairo_amd, w, h, ring, q, pframes, hot_records, e2e_records):
     ref = []
     tp = 0.0
     orc.op_counts(reset=True)
-    for t in range(pframes + 1):
+    for t in range(last + 1):
         rgb = cairo_amd.make_band4(w, h, t)
         t0 = time.perf_counter()
         data, n = e.encode(rgb)
         dt = time.perf_counter() - t0
-        if t > 0:
+        if 0 < t <= pframes:
             tp += dt
         ref.append(orc.canonical_frame_bytes(data, n, t == 0))
     base = {"value": round(w * h * pframes / tp / 1e6, 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
             "sample": f"{w}x{h} q={q} R={ring}: frame 0 (I, untimed) + {pframes} P-frames timed, band4 seed 1234, "
-                      f"oracle/evx_oracle.c -O2, one thread",
+                      f"oracle/evx_oracle.c -O3 -march=x86-64-v3, one thread",
             "cpu": cpu_model(), "host_cpus_available": host_cpus()}
 
     def compare(recs):
-        mism = [t for t in range(pframes + 1)
+        mism = [t for t in range(last + 1)
                 if t not in recs or orc.canonical_frame_bytes(recs[t][0], recs[t][1], t == 0) != ref[t]]
-        return {"frames_checked": pframes + 1, "mismatched_frames": mism}
+        return {"frames_checked": last + 1, "launches_covered": -(-(last + 1) // batch), "mismatched_frames": mism}
 
     hot = compare(hot_records)
     exact = {"hot_path_context": hot,
-             "what": "frames 0..n of the timed context (same batch, overlapping launches) serialized on the host, "
-                     "and of the end-to-end pipeline, vs the oracle's stream records (header byte 7 and tail bits "
-                     "masked)"}
+             "what": "frames 0..n of the timed context (same batch, overlapping launches: all of launch 0 and the "
+                     "head of launch 1) serialized on the host from the GPU-precoded feed, and of the end-to-end "
+                     "pipeline, vs the oracle's stream records (header byte 7 and tail bits masked)"}
     ok = not hot["mismatched_frames"]
     if e2e_records:
         exact["end_to_end_pipeline"] = compare(e2e_records)

@@ -84,6 +84,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_read_stamps": (I, [P, P]),
         "cairo_ctx_set_profiling": (I, [P, I]),
         "cairo_ctx_take_timings": (I, [P, P, ctypes.POINTER(I)]),
+        "cairo_ctx_busy_intervals": (I, [P, P, I, ctypes.POINTER(I)]),
         "cairo_ctx_set_workgroups": (I, [P, I]),
         "cairo_ctx_set_batch": (I, [P, I]),
         "cairo_ctx_peer_info": (I, [P, I, P]),
@@ -358,6 +359,14 @@ class Context:
         n = ctypes.c_int()
         _ck(self.L.cairo_ctx_take_timings(self.h, ms, ctypes.byref(n)), "take_timings")
         return list(ms), n.value
+
+    def busy_intervals(self) -> np.ndarray:
+        """(n, 2) engine launch [start, end) ms since profiling started, not reset."""
+        n = ctypes.c_int()
+        _ck(self.L.cairo_ctx_busy_intervals(self.h, None, 0, ctypes.byref(n)), "busy_intervals")
+        out = np.zeros((max(n.value, 1), 2), np.float64)
+        _ck(self.L.cairo_ctx_busy_intervals(self.h, _ptr(out), n.value, ctypes.byref(n)), "busy_intervals")
+        return out[: n.value]
 
     def set_batch(self, frames: int) -> None:
         _ck(self.L.cairo_ctx_set_batch(self.h, frames), "set_batch")

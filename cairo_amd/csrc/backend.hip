@@ -773,6 +773,26 @@ int cairo_ctx_take_timings(cairo_ctx* c, double ms[4], int* frames) {
   return kSuccess;
 }
 
+int cairo_ctx_busy_intervals(cairo_ctx* c, double* out, int cap, int* n) {
+  if (!c || !n || cap < 0 || (cap && !out)) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  CK(hipSetDevice(c->device));
+  int r = flush(c);
+  if (r) return r;
+  for (auto& t : c->tb) {
+    r = collect_times(c, t);
+    if (r) return r;
+  }
+  std::vector<std::pair<double, double>> iv = c->busy;
+  std::sort(iv.begin(), iv.end());
+  *n = (int)iv.size();
+  for (int i = 0; i < cap && i < (int)iv.size(); i++) {
+    out[2 * i] = iv[i].first;
+    out[2 * i + 1] = iv[i].second;
+  }
+  return kSuccess;
+}
+
 int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32_t index,
                      uint32_t type, uint32_t quality, int* ticket) {
   if (!c || !rgb || !ticket || quality < 1 || quality > 31 || type > 1) return kInvalidArg;

@@ -8,6 +8,8 @@
 // driven exp-Golomb codes), then a single loop codes it with the coder state
 // in registers, no division and no data-dependent branch per symbol; frames
 // are spread over host threads by the caller (pipeline.cpp).
+#include <immintrin.h>
+
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -75,34 +77,49 @@ struct CodeTables {
 const CodeTables kCodes;
 
 // Adaptive binary arithmetic coder, 16-bit precision (abac.cpp:28-348), run
-// over the whole feed of a slice in one loop with its state in registers.
+// over the whole feed of a slice with its state in registers.  The coder is
+// one serial chain per slice; everything here is about making that chain
+// short (about 14 dependent operations per symbol) and keeping the rest off
+// it.
 //
 // resolve_model's split floor(range * h0 / n), n = h0 + h1 (abac.cpp:78-93),
-// without a division on the serial chain: the model counts depend only on
-// the symbols, so the fixed-point ratio M = h0 * 2^47 / n (rounded up by
-// 1..3 units) is computed beside the chain, and the split is one multiply:
-// floor(range * M / 2^47).  Exact while 3 * 2^16 * n < 2^47 (n < 7e8; a slice
-// has at most 8 feed sections of 32 Mbit, n < 2^28): the overshoot
-// range * (M - h0 2^47 / n) / 2^47 stays below 1/n, the smallest nonzero
-// fractional part of range * h0 / n, and M >= h0 2^47 / n keeps exact
+// without a division on the chain: the model counts depend only on the
+// symbols, so the fixed-point ratio M = h0 * 2^47 / n (rounded up by 1..3
+// units) is precomputed for a block of symbols (vectorized), and the split is
+// one multiply: floor(range * M / 2^47).  Exact while 3 * 2^16 * n < 2^47
+// (n < 7e8; a slice has at most 8 feed sections of 32 Mbit, n < 2^28): the
+// overshoot range * (M - h0 2^47 / n) / 2^47 stays below 1/n, the smallest
+// nonzero fractional part of range * h0 / n, and M >= h0 2^47 / n keeps exact
 // quotients.  The double estimate of h0 2^47 / n is within 2^-4 of the true
 // value, so floor(estimate) + 2 overshoots by 1..2.0625.
 //
-// resolve_encode_scaling (abac.cpp:178-224) is done in closed form, without
-// data-dependent branches (the bits are close to random, so a loop or an
-// if per output bit mispredicts about once per symbol):
-//  * shift-out: the k = clz16(low ^ high) common leading bits leave MSB first;
-//    pending underflow bits (e3, the opposite of the first one) follow the
-//    first of them;
-//  * underflow (E3): then, while low = 01.. and high = 10.., bit 14 is
-//    removed from both; that is the run of leading ones of low & ~high from
-//    bit 14, cut short where the reference's bound high <= 0xBFFD (not
-//    0xBFFF) stops it: high = 0xBFFE at the first step, or bits 13..0 of
-//    high all ones once its trailing ones reach them.
+// The symbol: b is known in advance, so both outcomes are formed from the
+// state at the start of the step and one select (cmov) picks each value:
+//   b = 0: l1 = low,     h1 = mid,   r' = t              (mid = low + t)
+//   b = 1: l1 = mid + 1, h1 = high,  r' = r - t - 1      (r = high - low)
+// resolve_encode_scaling (abac.cpp:178-224) in closed form, without a
+// data-dependent branch per symbol:
+//  * E1/E2 shift-out: k = clz16(l1 ^ h1) common leading bits leave MSB first;
+//    pending underflow bits (e3 copies of the opposite of the first one)
+//    follow the first of them;
+//  * E3 (underflow): then, while low = 01.. and high = 10.., bit 14 is removed
+//    from both: the run of (l = 1, h = 0) just below the first differing bit,
+//    i.e. the leading zeros of ~((l1 & ~h1) << 1) shifted by 16 + k.  The
+//    reference's bound is high <= 0xBFFD, not 0xBFFF: high = 0xBFFE at the
+//    first step, or bits 13..0 of high all ones once its trailing ones reach
+//    them, stops the run early.  That needs many trailing ones (about one
+//    symbol in 10^4), so it is a predicted branch off the chain.
+//  * with s = k + E3 steps in all, low' = (l1 << s) & 0x7FFF and the range
+//    is ((r' + 1) << s) - 1: the shifted-out bits of h1 and l1 differ by
+//    exactly one unit of 2^15 (common bits cancel; the first differing bit
+//    1/0 and the E3 run 0../1.. leave 1).  high = low + range is derived off
+//    the chain.
 //
-// Output bits collect MSB-first in a 64-bit accumulator; each full 32 are
-// bit-reversed into bit_stream order (LSB first, bitstream.cpp:181-245) and
-// stored to a scratch buffer with slack.  `s0` bits of the caller's first
+// Output bits (b0, the e3 run of !b0, b1..b(k-1) = W + 2^(len-1) - 2^(k-1)
+// for W = the top k bits of l1) collect MSB first in a 64-bit accumulator; a
+// 32-bit word is stored every step (the store pointer advances when it is
+// full, no branch) and the words are bit-reversed into bit_stream order (LSB
+// first, bitstream.cpp:181-245) at the end.  `s0` bits of the caller's first
 // byte are preloaded.  Returns the number of bits in `buf` (including the s0
 // preloaded ones; the buffer holds them rounded up to 4 bytes), or ~0 once
 // the output passes `limit`.
@@ -113,72 +130,113 @@ inline uint32_t rev32(uint32_t x) {
   return ((x & 0x55555555u) << 1) | ((x >> 1) & 0x55555555u);
 }
 
+constexpr uint32_t kSplitBlock = 4096;  // symbols whose split ratios are precomputed together
+
+// M for symbols i = 0..len-1 of a block: h0 before symbol i is h[i], n = n0 + i.
+inline uint64_t split_ratio(int32_t h0, uint32_t n) {
+  return (uint64_t)(int64_t)((double)h0 * (140737488355328.0 / (double)(int32_t)n)) + 2;  // 2^47
+}
+void splits_scalar(const int32_t* h, uint32_t n0, uint32_t len, uint64_t* out) {
+  for (uint32_t i = 0; i < len; i++) out[i] = split_ratio(h[i], n0 + i);
+}
+__attribute__((target("avx512f,avx512dq"))) void splits_avx512(const int32_t* h, uint32_t n0, uint32_t len,
+                                                                uint64_t* out) {
+  const __m512d two47 = _mm512_set1_pd(140737488355328.0);
+  const __m512d iota = _mm512_setr_pd(0, 1, 2, 3, 4, 5, 6, 7);
+  const __m512i two = _mm512_set1_epi64(2);
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {  // the same IEEE operations as split_ratio, 8 at a time
+    const __m512d nd = _mm512_add_pd(_mm512_set1_pd((double)(n0 + i)), iota);
+    const __m512d hd = _mm512_cvtepi32_pd(_mm256_loadu_si256((const __m256i*)(h + i)));
+    const __m512d q = _mm512_mul_pd(hd, _mm512_div_pd(two47, nd));
+    _mm512_storeu_si512((__m512i*)(out + i), _mm512_add_epi64(_mm512_cvttpd_epi64(q), two));
+  }
+  splits_scalar(h + i, n0 + i, len - i, out + i);
+}
+const bool kHaveAvx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq");
+
 uint64_t abac_encode(const uint64_t* feed, uint64_t nbits, uint8_t first, uint32_t s0, uint8_t* buf,
                      const uint8_t* limit) {
-  uint32_t low = 0, high = 0xFFFF, e3 = 0, h0 = 1, n = 2;
+  uint32_t low = 0, high = 0xFFFF, r = 0xFFFF, e3 = 0, h0 = 1, n = 2;
+  uint32_t low1 = 1, nlow = ~0u, nlowm1 = ~0u - 1;  // low + 1, ~low, ~low - 1
   uint64_t macc = 0;  // pending output, MSB first: the oldest of the mn bits is bit mn-1
   uint32_t mn = 0;
-  uint8_t* p = buf;
-  auto spill = [&]() {  // mn >= 32
-    mn -= 32;
-    const uint32_t w = rev32((uint32_t)(macc >> mn));
-    memcpy(p, &w, 4);
-    p += 4;
-  };
+  uint32_t* p = reinterpret_cast<uint32_t*>(buf);  // 32-bit words, MSB-first until the final reversal
+  const uint32_t* const plimit = reinterpret_cast<const uint32_t*>(buf + ((limit - buf) & ~(ptrdiff_t)3));
+  alignas(64) int32_t hbuf[kSplitBlock];
+  alignas(64) uint64_t mbuf[kSplitBlock];
   auto put1 = [&](uint32_t bit) {
     macc = (macc << 1) | bit;
-    if (++mn >= 32) spill();
+    if (++mn >= 32) {
+      mn -= 32;
+      *p++ = (uint32_t)(macc >> mn);
+    }
   };
   for (uint32_t i = 0; i < s0; i++) put1((first >> i) & 1u);
-  for (uint64_t base = 0; base < nbits; base += 64) {
-    const uint64_t word = feed[base >> 6];
-    const uint32_t cnt = nbits - base < 64 ? (uint32_t)(nbits - base) : 64u;
-    if (p >= limit) return ~0ull;  // a word emits at most 64 * 32 bits: the slack absorbs it
-    for (uint32_t j = 0; j < cnt; j++) {
-      const uint32_t b = (uint32_t)(word >> j) & 1u;
-      const uint32_t sel = 0u - b;  // all ones for a 1 (masks, not ?: -- gcc turns those into branches)
-      const uint64_t m = (uint64_t)(int64_t)((double)(int32_t)h0 * (140737488355328.0 / (double)(int32_t)n)) + 2;  // 2^47
-      const uint32_t mid = low + (uint32_t)(((uint64_t)(high - low) * m) >> 47);  // resolve_model
-      n++;
-      h0 += b ^ 1u;
-      low = (low & ~sel) | ((mid + 1) & sel);
-      high = (high & sel) | (mid & ~sel);
-      // shift-out of the k common leading bits: b0, e3 copies of !b0, b1..b(k-1)
-      const uint32_t k = (uint32_t)__builtin_clz(((low ^ high) << 16) | 0x8000u);  // 0..16
-      if (__builtin_expect(e3 > 16, 0)) {
-        for (uint32_t i = 0; i < k; i++) {
-          const uint32_t bit = (low >> (15 - i)) & 1u;
+  for (uint64_t c0 = 0; c0 < nbits; c0 += kSplitBlock) {
+    const uint32_t clen = nbits - c0 < kSplitBlock ? (uint32_t)(nbits - c0) : kSplitBlock;
+    const uint64_t* fw = feed + (c0 >> 6);
+    {
+      uint32_t hh = h0;
+      for (uint32_t i = 0; i < clen; i++) {
+        hbuf[i] = (int32_t)hh;
+        hh += (uint32_t)((~fw[i >> 6] >> (i & 63)) & 1u);
+      }
+      if (kHaveAvx512)
+        splits_avx512(hbuf, n, clen, mbuf);
+      else
+        splits_scalar(hbuf, n, clen, mbuf);
+      h0 = hh;
+      n += clen;
+    }
+    for (uint32_t i = 0; i < clen; i++) {
+      if ((i & 63) == 0 && p >= plimit) return ~0ull;  // 64 symbols emit at most 64 * 32 bits: the slack absorbs it
+      const uint32_t b = (uint32_t)(fw[i >> 6] >> (i & 63)) & 1u;
+      const uint32_t t = (uint32_t)(((uint64_t)r * mbuf[i]) >> 47);  // resolve_model: mid = low + t
+      uint32_t l1 = low, h1 = low + t, rp1 = t + 1, ny = 2 * (h1 | nlow) + 1;  // ny = ~((l1 & ~h1) << 1)
+      const uint32_t l1b = low1 + t, rp1b = r - t, nyb = 2 * (high | (nlowm1 - t)) + 1;
+      asm("test %[b], %[b]\n\tcmovnz %[l1b], %[l1]\n\tcmovnz %[hb], %[h1]\n\tcmovnz %[rb], %[rp]\n\tcmovnz %[nb], %[ny]"
+          : [l1] "+&r"(l1), [h1] "+&r"(h1), [rp] "+&r"(rp1), [ny] "+&r"(ny)
+          : [b] "r"(b), [l1b] "r"(l1b), [hb] "r"(high), [rb] "r"(rp1b), [nb] "r"(nyb)
+          : "cc");
+      const uint32_t k16 = _lzcnt_u32(l1 ^ h1);  // 16 + k, k = 0..16
+      const uint32_t k = k16 - 16;
+      uint32_t s = k16 + _lzcnt_u32(ny << (k16 & 31)) - 16;  // k + the E3 run
+      {  // the 0xBFFD bound (rare)
+        uint32_t tz = _tzcnt_u32(~h1);
+        tz = h1 == 0xBFFEu ? 14u : tz;
+        const int32_t bound = 14 - (int32_t)tz;
+        const uint32_t X = (int32_t)k > bound ? k : (uint32_t)bound;
+        if (__builtin_expect(X < s, 0)) s = X;
+      }
+      if (__builtin_expect(e3 > 16, 0)) {  // a long pending run: bit by bit
+        for (uint32_t j = 0; j < k; j++) {
+          const uint32_t bit = (l1 >> (15 - j)) & 1u;
           put1(bit);
-          for (; i == 0 && e3; e3--) {
+          for (; j == 0 && e3; e3--) {
             put1(bit ^ 1u);
-            if (p >= limit) return ~0ull;
+            if (p >= plimit) return ~0ull;
           }
         }
       } else {
-        const uint32_t kmask = 0u - (uint32_t)(k != 0);
-        const uint32_t nrun = e3 & kmask;
-        const uint32_t top = low >> (16 - k);  // 0 for k = 0
-        const uint64_t b0 = (low >> 15) & 1u & kmask;
-        const uint64_t run = ((1ull << nrun) - 1) & (b0 - 1);
+        const uint32_t nrun = e3 & (0u - (uint32_t)(k != 0));
         const uint32_t len = k + nrun;  // <= 32
-        macc = (macc << len) | (b0 << ((len - 1) & 63)) | (run << ((k - 1) & 63)) | (top & (((1u << k) - 1u) >> 1));
+        const uint64_t W = l1 >> (16 - k);
+        macc = (macc << len) | (W + (1ull << ((len - 1) & 63)) - (1ull << ((k - 1) & 63)));
         mn += len;
         e3 -= nrun;
-        if (mn >= 32) spill();
+        const uint32_t full = mn >= 32;
+        *p = (uint32_t)(macc >> ((mn - 32) & 63));
+        p += full;
+        mn -= full << 5;
       }
-      // underflow, from the unshifted values: the run of low = 1 / high = 0
-      // starting just below the first differing bit (bit 14 - k)
-      const uint64_t y = low & ~high;
-      const uint32_t sh = k + 49 < 63 ? k + 49 : 63;
-      uint32_t m3 = (uint32_t)__builtin_clzll(~(y << sh));
-      uint32_t t = k + (uint32_t)__builtin_ctz(~high);  // trailing ones of high after the shift-out
-      t = t < 16 ? t : 16;
-      const uint32_t lim = (14u - t) & (0u - (uint32_t)(t < 14)) & (0u - (uint32_t)((high | k) != 0xBFFEu));
-      m3 = m3 < lim ? m3 : lim;
-      e3 += m3;
-      const uint32_t s = k + m3;
-      low = (low << s) & 0x7FFFu;
-      high = 0x8000u | ((high << s) & 0x7FFFu) | ((1u << s) - 1u);
+      e3 += s - k;
+      r = (rp1 << s) - 1;
+      low = (l1 << s) & 0x7FFFu;
+      high = low + r;
+      low1 = low + 1;
+      nlow = ~low;
+      nlowm1 = nlow - 1;
     }
   }
   // flush_encoder (abac.cpp:279-310)
@@ -187,11 +245,11 @@ uint64_t abac_encode(const uint64_t* feed, uint64_t nbits, uint8_t first, uint32
   put1(fb);
   for (; e3; e3--) {
     put1(fb ^ 1u);
-    if (p >= limit) return ~0ull;
+    if (p >= plimit) return ~0ull;
   }
-  const uint64_t total = (uint64_t)(p - buf) * 8 + mn;
-  const uint32_t w = mn ? rev32((uint32_t)(macc << (32 - mn))) : 0u;
-  memcpy(p, &w, 4);
+  const uint64_t total = (uint64_t)(p - reinterpret_cast<uint32_t*>(buf)) * 32 + mn;
+  *p = mn ? (uint32_t)(macc << (32 - mn)) : 0u;
+  for (uint32_t* q = reinterpret_cast<uint32_t*>(buf); q <= p; q++) *q = rev32(*q);
   return total;
 }
 

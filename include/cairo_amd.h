@@ -143,6 +143,11 @@ CAIRO_API int cairo_ctx_set_profiling(cairo_ctx *ctx, int enable);
  * accumulators.  Enabling profiling starts the common clock of the busy
  * intervals. */
 CAIRO_API int cairo_ctx_take_timings(cairo_ctx *ctx, double ms[4], int *frames);
+/* The engine launches' [start, end) intervals (ms on the profiling clock,
+ * pairs, sorted by start) collected since the last cairo_ctx_take_timings,
+ * without resetting them: the busy-time union can be recomputed from them.
+ * *n receives the count; at most cap pairs are written. */
+CAIRO_API int cairo_ctx_busy_intervals(cairo_ctx *ctx, double *out, int cap, int *n);
 /* Row-coder workgroups of the engine per launch (0 = automatic: a quarter of
  * the device's resident engine workgroups, 192 on a full MI355X; larger
  * values are rejected, since every launch must stay co-resident with the

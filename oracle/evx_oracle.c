@@ -821,6 +821,21 @@ static void abac_flush(abac *a, obits *o) {
     abac_clear(a);
 }
 
+/* The coder alone over a raw feed (LSB-first 32-bit words), one slice:
+ * encode_symbol per bit, then flush_encoder (abac.cpp:110-135, 178-224,
+ * 279-310).  Test infrastructure: checks the product's closed-form coder on
+ * arbitrary bit sequences.  Returns the bits written (0 with *err set if
+ * they exceed cap_bits). */
+uint32_t orc_abac_feed(const uint32_t *words, uint64_t nbits, uint8_t *out, uint32_t cap_bits, int *err) {
+    abac a;
+    abac_clear(&a);
+    obits o = {out, cap_bits, 0, 0};
+    for (uint64_t i = 0; i < nbits; i++) abac_bit(&a, (words[i >> 5] >> (i & 31)) & 1u, &o);
+    abac_flush(&a, &o);
+    if (err) *err = o.err;
+    return o.w;
+}
+
 /* The feed stream (common.cpp:147) only bounds how many bits one section may
  * write between empty() calls; every accepted bit is consumed by the coder
  * in order.  Writes that would exceed capacity are dropped whole

@@ -83,6 +83,8 @@ void orc_make_frame(uint8_t *rgb, int w, int h, uint32_t t, uint32_t seed);
 void orc_op_counts(uint64_t out[4], int reset);
 /* FNV-1a-64 over bytes, continuing from h. */
 uint64_t orc_fnv1a64(uint64_t h, const uint8_t *data, uint64_t n);
+/* the arithmetic coder alone over a raw LSB-first feed (one slice + flush) */
+uint32_t orc_abac_feed(const uint32_t *words, uint64_t nbits, uint8_t *out, uint32_t cap_bits, int *err);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,8 @@ def lib() -> ctypes.CDLL:
         L.orc_make_frame.argtypes = [P, I, I, U, U]
         L.orc_fnv1a64.restype = ctypes.c_uint64
         L.orc_fnv1a64.argtypes = [ctypes.c_uint64, P, ctypes.c_uint64]
+        L.orc_abac_feed.restype = U
+        L.orc_abac_feed.argtypes = [P, ctypes.c_uint64, P, U, ctypes.POINTER(I)]
         L.orc_transform_8x8.argtypes = [P, I, P, I]
         L.orc_sub_transform_8x8.argtypes = [P, I, P, I, P, I]
         L.orc_inverse_transform_8x8.argtypes = [P, I, P, I]
@@ -181,3 +183,14 @@ class OracleEncoder:
         d = np.frombuffer(ctypes.string_at(self.L.orc_inter_descs(self.h), n * 16), BLOCK_DESC).copy()
         s = np.frombuffer(ctypes.string_at(self.L.orc_inter_sads(self.h), n * 4), np.int32).copy()
         return d, s
+
+
+def abac_feed(words: np.ndarray, nbits: int) -> tuple[bytes, int]:
+    """The reference coder (abac.cpp) alone over a raw LSB-first feed -> (bytes, bits)."""
+    w = np.ascontiguousarray(words, dtype=np.uint32)
+    cap = nbits * 2 + 4096
+    out = np.zeros(cap // 8 + 8, np.uint8)
+    err = ctypes.c_int(0)
+    n = lib().orc_abac_feed(_ptr(w), nbits, _ptr(out), cap, ctypes.byref(err))
+    assert not err.value
+    return out[: (n + 7) // 8].tobytes(), int(n)
