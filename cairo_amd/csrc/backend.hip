@@ -101,6 +101,13 @@ struct cairo_ctx {
   size_t plane_elems = 0, mbs = 0, nref = 1;
   hipStream_t ks = nullptr, cs = nullptr;
   hipStream_t ks2 = nullptr;         // launches alternate between ks and ks2 (consecutive batches overlap)
+  // Host RGB uploads (rgb_on_device = 0), issued at submit on a stream of
+  // their own so that they overlap the launches in flight; a launch waits for
+  // the last one (the stream is in order).  Made on first use; a group member
+  // keeps uploading on its launch stream (its queue budget, join_group).
+  hipStream_t us = nullptr;
+  hipEvent_t up_last = nullptr;
+  bool up_pending = false;  // an upload the next launch has not waited for
   hipEvent_t engine_done = nullptr;  // last launched batch finished (copy stream waits on it)
   hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k (every task done)
   hipEvent_t batch_ready[kSyncAreas] = {};  // its frames converted, views and sync area set up
@@ -120,6 +127,7 @@ struct cairo_ctx {
   int16_t* ring_buf = nullptr;
   uint64_t* progress = nullptr;  // [stages][hmb] tagged deblock progress of each slot's frame
   bool fresh = true;             // no frame since create / reset: the next has no predecessor
+  long since_fresh = 0;          // frames since create / reset (frame_links)
   // Frame-interleaved group (cairo_ctx_join_group): member grank of gsize
   // encodes the stream's frames n = grank (mod gsize), reading the others'
   // reconstructions, output_cache and progress words in place.
@@ -309,6 +317,9 @@ void free_ctx(cairo_ctx* c) {
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps})
     (void)hipFree(p);
+  if (c->us) (void)hipStreamSynchronize(c->us);
+  if (c->up_last) (void)hipEventDestroy(c->up_last);
+  if (c->us) (void)hipStreamDestroy(c->us);
   if (c->ks) (void)hipStreamDestroy(c->ks);
   if (c->ks2) (void)hipStreamDestroy(c->ks2);
   if (c->cs) (void)hipStreamDestroy(c->cs);
@@ -339,6 +350,7 @@ int zero_state(cairo_ctx* c) {
   c->batches = 0;
   c->prev_total = 0;  // its sync areas are zero now
   c->fresh = true;  // the first frame after a reset depends on no earlier frame
+  c->since_fresh = 0;
   // tickets restart at 0 (every stage is idle here): a group member's k-th
   // frame after a (re)join is its ticket k, which its peers assume when they
   // locate its output_cache and progress words (frame_links)
@@ -424,6 +436,10 @@ int flush(cairo_ctx* c) {
     c->tb_next = (c->tb_next + 1) % kLaunchSlots;
     int r = collect_times(c, *tb);  // its events are about to be reused
     if (r) return r;
+  }
+  if (c->up_pending) {  // the frames' uploads, issued at submit on the upload stream
+    CK(hipStreamWaitEvent(st, c->up_last, 0));
+    c->up_pending = false;
   }
   for (int i = 0; i < e.nframes; i++) {  // host RGB sources; the decoder's table and coefficients
     const FrameDesc& f = c->pend[i];
@@ -551,7 +567,14 @@ void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
       f.coef_prev = zero;
       f.prev_progress = nullptr;
     }
+    if (n >= 2) {
+      const cairo_ctx::Peer& p = c->gp[(n - 2) % N];
+      f.prev2_progress = p.progress + (size_t)(((n - 2) / N) % p.stages) * c->hmb;
+    } else {
+      f.prev2_progress = nullptr;
+    }
     c->fresh = false;
+    c->since_fresh++;
     return;
   }
   for (int k = 0; k < kMaxRing; k++)
@@ -561,7 +584,9 @@ void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
   f.coef_prev = slot_planes(c->coef, c, ps);
   f.progress = c->progress + (size_t)f.slot * c->hmb;
   f.prev_progress = c->fresh ? nullptr : c->progress + (size_t)ps * c->hmb;
+  f.prev2_progress = c->since_fresh < 2 ? nullptr : c->progress + (size_t)((t + 2 * c->stages - 2) % c->stages) * c->hmb;
   c->fresh = false;
+  c->since_fresh++;
 }
 
 int sync_all(cairo_ctx* c) {
@@ -571,6 +596,7 @@ int sync_all(cairo_ctx* c) {
   CK(hipStreamSynchronize(c->ks2));
   CK(hipStreamSynchronize(c->cs));
   if (c->ps) CK(hipStreamSynchronize(c->ps));
+  if (c->us) CK(hipStreamSynchronize(c->us));
   return kSuccess;
 }
 
@@ -818,9 +844,19 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   if (rgb_on_device) {
     f.rgb = rgb;
     f.host_rgb = nullptr;
-  } else {  // uploaded at launch, on the launch's stream (the caller keeps it valid until wait)
+  } else {  // the caller keeps it valid until wait
     f.rgb = c->rgb + (size_t)slot * c->w * c->h * 3;
     f.host_rgb = rgb;
+    if (c->gsize == 1) {  // uploaded now, beside the launches in flight (the slot's last reader is done: released)
+      if (!c->us) {
+        CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
+        CK(hipEventCreateWithFlags(&c->up_last, hipEventDisableTiming));
+      }
+      CK(hipMemcpyAsync((void*)f.rgb, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, c->us));
+      CK(hipEventRecord(c->up_last, c->us));
+      c->up_pending = true;
+      f.host_rgb = nullptr;
+    }
   }
   if (c->gsize > 1 && (long)index != (long)(t - c->gbase) * c->gsize + c->grank) {
     fprintf(stderr, "[cairo_amd] group member %d of %d: frame %u out of turn\n", c->grank, c->gsize, index);

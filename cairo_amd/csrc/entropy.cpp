@@ -12,6 +12,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "../../include/cairo_amd.h"
@@ -345,9 +346,15 @@ int code_feed(const uint64_t* feed, uint64_t nbits, uint8_t* out, uint64_t out_b
   // untouched.
   const uint64_t byte0 = pos0 >> 3, cap_bytes = (out_bits_capacity + 7) / 8 - byte0;
   constexpr uint64_t kSlack = 512;  // > the output of one 64-symbol feed word
-  thread_local std::vector<uint8_t> scratch;
-  if (scratch.size() < cap_bytes + kSlack) scratch.resize(cap_bytes + kSlack);
-  uint8_t* const buf = scratch.data();
+  // scratch for the coder's word stores: grown without zero-filling (a 4K
+  // caller's bit_stream may offer 66 MB; only the pages written are touched)
+  thread_local std::unique_ptr<uint32_t[]> scratch;
+  thread_local uint64_t scratch_bytes = 0;
+  if (scratch_bytes < cap_bytes + kSlack) {
+    scratch_bytes = (cap_bytes + kSlack + 4095) & ~(uint64_t)4095;
+    scratch.reset(new uint32_t[scratch_bytes / 4]);
+  }
+  uint8_t* const buf = reinterpret_cast<uint8_t*>(scratch.get());
   const uint32_t s0 = (uint32_t)(pos0 & 7);
   const uint64_t total = abac_encode(feed, nbits, s0 ? out[byte0] : 0, s0, buf, buf + cap_bytes);
   if (total == ~0ull || byte0 * 8 + total > out_bits_capacity) return 7;  // EVX_ERROR_CAPACITY_LIMIT

@@ -74,6 +74,7 @@ struct FrameDesc {
   PlaneSet coef_prev;        // the previous frame's output_cache (copy-macroblock chain)
   uint64_t* progress;        // this frame's deblock progress words [hmb]
   const uint64_t* prev_progress;  // the previous frame's (nullptr: none, first frame after a reset)
+  const uint64_t* prev2_progress;  // frame index-2's (nullptr: none)
   int sys;                   // FrameArgs::sys
   const BlockDesc* host_table;  // decode: the frame's block table and coefficient planes (y, u, v
   const int16_t* host_coef;     //   contiguous), uploaded at launch
@@ -118,6 +119,9 @@ struct FrameArgs {
   // earlier frame is final there), so no launch ordering guards them.
   uint64_t* progress;             // [hmb] this frame's
   const uint64_t* prev_progress;  // [hmb] the previous frame's (nullptr: none)
+  // [hmb] frame index-2's (nullptr: none): the searches of the older
+  // references (offsets 2..R-1) wait on it instead of the previous frame
+  const uint64_t* prev2_progress;
   // 1: the cross-frame buffers are shared with other devices or processes (a
   // frame-interleaved group): progress words are stored and polled at system
   // scope, with a system-scope release before each store and a system-scope

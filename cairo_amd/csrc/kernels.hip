@@ -688,18 +688,20 @@ __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState&
 __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st);
 __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st);
 
-// Helper wait (whole workgroup): until the previous frame's deblock progress
-// of MB row rr reaches need, running this row's ready deblock chunks
-// meanwhile; then acquire what the progress word released.  Bounded like
-// every wait (the error word ends it).
-__device__ __forceinline__ void helper_wait(FA& a, int r, int rr, int need, DbLds& D,
+// Helper wait (whole workgroup): until the deblock progress of frame
+// index-back (back = 1: the previous frame, 2: the one before) of MB row rr
+// reaches need, running this row's ready deblock chunks meanwhile; then
+// acquire what the progress word released.  Bounded like every wait (the
+// error word ends it).
+__device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int need, DbLds& D,
                                             DbState& st, int* flag) {
   volatile int* vflag = flag;
+  const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
   uint64_t t0 = 0;
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
-      if (!a.prev_progress || progress_peer(a.sys, a.prev_progress + rr) >= tagged(a.epoch - 1, need)) {
+      if (!pp || progress_peer(a.sys, pp + rr) >= tagged(a.epoch - back, need)) {
         d = 1;
       } else if (kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
         d = 2;
@@ -792,7 +794,8 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
         lvl2_open = (m4 >> 2) != 0;
         if (m) {
           if (is) is[5] = __builtin_amdgcn_s_memrealtime();
-          helper_wait(a, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2), D, st, flag);
+          helper_wait(a, off == 1 ? 1 : 2, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2), D, st,
+                      flag);
           if (m & 2) load_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
           if (!lvl2c) load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
           __syncthreads();
@@ -1897,12 +1900,21 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     trace(tr, 2, (int)a.epoch * 1000 + r);
     uint64_t* is = a.istamps && tid == 0 ? a.istamps + (size_t)(r * a.ng + g) * kIStamps : nullptr;
     if (is) is[0] = __builtin_amdgcn_s_memrealtime(), is[3] = is[4] = is[5] = is[6] = is[7] = is[8] = is[9] = is[10] = 0;
-    // level 1 of the group's window (inter_task); deblock meanwhile
-    helper_wait(a, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+    // The older references (offsets 2..R-1) first: frame index-2 is final
+    // over the group's level-1 window long before the previous frame is (its
+    // progress word, tagged epoch-2, also covers frame index-3: that frame's
+    // row r+2 waited for index-3's row r+4 over a wider window), so these
+    // searches fill what used to be the wait for the previous frame.
+    if (a.inter && a.nref >= 2) {
+      helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+      for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is);
+    }
+    // level 1 of the group's window in the previous frame; deblock meanwhile
+    helper_wait(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
-      for (int off = 1; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is);
+      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is);
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2098,6 +2110,7 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, a.ng, j);
   a.progress = f.progress;
   a.prev_progress = f.prev_progress;
+  a.prev2_progress = f.prev2_progress;
   a.sys = f.sys;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   {
