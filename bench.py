@@ -479,9 +479,9 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
 
     def make():
         nonlocal ctx
-        # two launches' worth of staging slots: every member imports the
-        # others' output_cache slots over IPC, so they are kept small
-        ctx = share(cairo_amd.Context(w, h, ring, device=local, stages=a.stages or 2 * batch))
+        # the library's staging slots (96): every member imports the others'
+        # output_cache over IPC, exported in chunks below 1 GiB each
+        ctx = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
         ctx.set_batch(batch)
         ctx.set_outputs(cairo_amd.OUT_FEED)
 

@@ -38,7 +38,8 @@ assert BLOCK_DESC.itemsize == 16
 EVX_SUCCESS = 0
 OUT_COEF, OUT_FEED = 1, 2  # cairo_ctx_set_outputs
 FEED_NONE, FEED_VALID, FEED_OVERFLOW = 0, 1, 2
-PEER_SIZE = 3 * 4 + 5 * 4 + 3 * 8 + 3 * 64  # sizeof(cairo_peer)
+MAX_COEF_CHUNKS = 16  # CAIRO_MAX_COEF_CHUNKS
+PEER_SIZE = 3 * 4 + 7 * 4 + 2 * 8 + MAX_COEF_CHUNKS * 8 + 2 * 64 + MAX_COEF_CHUNKS * 64  # sizeof(cairo_peer)
 # EVX_PEEK_STATE (reference evx1.h:55-64)
 PEEK_SOURCE, PEEK_PREDICTION, PEEK_BLOCK_TABLE, PEEK_QUANT_TABLE, PEEK_SPMP_TABLE, PEEK_BLOCK_VARIANCE, \
     PEEK_DESTINATION = range(7)
@@ -90,6 +91,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_peer_info": (I, [P, I, P]),
         "cairo_ctx_join_group": (I, [P, I, I, P]),
         "cairo_group_check_queues": (I, [I]),
+        "cairo_peer_size": (I, []),
         "cairo_ctx_flush": (I, [P]),
         "cairo_ctx_set_helpers": (I, [P, I]),
         "cairo_ctx_max_workgroups": (I, [P]),

@@ -55,6 +55,10 @@ inline int default_batch(size_t mbs) {
   return mbs <= (size_t)kMidFrameMBs ? 32 : 28;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
+// The output_cache slots are allocated in chunks of at most this size, each
+// exported with its own IPC handle (cairo_peer): an IPC import of one
+// fine-grained allocation of 2 GiB or more never returned.
+constexpr size_t kCoefChunkBytes = size_t(1) << 30;
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)
               kInvalidResource = 8;
 
@@ -119,7 +123,9 @@ struct cairo_ctx {
   int order_slope = kOrderSlope;  // of the task order tables (3N + 2 in an N-member group)
   long long batches = 0;             // launches so far
   // per-slot device buffers
-  int16_t *src = nullptr, *coef = nullptr;
+  int16_t* src = nullptr;
+  int16_t* coef[CAIRO_MAX_COEF_CHUNKS] = {};  // output_cache: slot s in chunk s / coef_per, at s % coef_per
+  int coef_chunks = 0, coef_per = 0;
   BlockDesc *table = nullptr, *idesc = nullptr;
   int32_t* isad = nullptr;
   uint64_t* gran = nullptr;
@@ -133,7 +139,8 @@ struct cairo_ctx {
   // reconstructions, output_cache and progress words in place.
   struct Peer {
     int16_t* ring = nullptr;
-    int16_t* coef = nullptr;
+    int16_t* coef[CAIRO_MAX_COEF_CHUNKS] = {};
+    int coef_chunks = 0, coef_per = 1;
     uint64_t* progress = nullptr;
     int stages = 0;
     bool imported = false;  // opened from another process's IPC handles
@@ -219,6 +226,37 @@ PlaneSet planes_at(int16_t* base, const cairo_ctx* c) {
 PlaneSet slot_planes(int16_t* base, const cairo_ctx* c, int slot) {
   return ring_slot(base, c->plane_elems, (int)c->wa, (int)c->ha, slot);
 }
+// Staging slot s's output_cache (chunked allocation).
+int16_t* coef_base(const cairo_ctx* c, int slot) {
+  return c->coef[slot / c->coef_per] + (size_t)(slot % c->coef_per) * c->plane_elems;
+}
+PlaneSet coef_planes(const cairo_ctx* c, int slot) { return planes_at(coef_base(c, slot), c); }
+PlaneSet peer_coef_planes(const cairo_ctx::Peer& p, const cairo_ctx* c, int slot) {
+  return planes_at(p.coef[slot / p.coef_per] + (size_t)(slot % p.coef_per) * c->plane_elems, c);
+}
+// Allocate the output_cache chunks (fine-grained for cross-device sharing);
+// on failure nothing stays allocated.
+hipError_t alloc_coef(const cairo_ctx* c, bool fine, int16_t* out[CAIRO_MAX_COEF_CHUNKS], int* chunks, int* per) {
+  const size_t slot_bytes = c->plane_elems * 2;
+  const int p = (int)std::max<size_t>(1, std::min<size_t>((size_t)c->stages, kCoefChunkBytes / slot_bytes));
+  const int n = (c->stages + p - 1) / p;
+  if (n > CAIRO_MAX_COEF_CHUNKS) return hipErrorInvalidValue;
+  for (int k = 0; k < CAIRO_MAX_COEF_CHUNKS; k++) out[k] = nullptr;
+  for (int k = 0; k < n; k++) {
+    const size_t bytes = slot_bytes * (size_t)std::min(p, c->stages - k * p);
+    const hipError_t e = fine ? hipExtMallocWithFlags((void**)&out[k], bytes, hipDeviceMallocFinegrained)
+                              : hipMalloc((void**)&out[k], bytes);
+    if (e != hipSuccess) {
+      for (int j = 0; j <= k; j++)
+        if (out[j]) (void)hipFree(out[j]);
+      for (int j = 0; j < CAIRO_MAX_COEF_CHUNKS; j++) out[j] = nullptr;
+      return e;
+    }
+  }
+  *chunks = n;
+  *per = p;
+  return hipSuccess;
+}
 
 size_t stamp_words(const cairo_ctx* c) {
   // frames, engine entry/exit, then 3 stamps per inter task
@@ -232,7 +270,6 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.wa = (int)c->wa, e.ha = (int)c->ha, e.w = (int)c->w, e.h = (int)c->h;
   e.wmb = (int)c->wmb, e.hmb = (int)c->hmb, e.ring = (int)c->ring;
   e.src_base = c->src;
-  e.coef_base = c->coef;
   e.plane_elems = c->plane_elems;
   e.table_base = c->table;
   e.idesc_base = c->idesc;
@@ -251,8 +288,10 @@ void leave_group(cairo_ctx* c) {
   for (int i = 0; i < c->gsize; i++) {
     cairo_ctx::Peer& p = c->gp[i];
     if (p.imported) {
-      for (void* q : {(void*)p.ring, (void*)p.coef, (void*)p.progress})
+      for (void* q : {(void*)p.ring, (void*)p.progress})
         if (q) (void)hipIpcCloseMemHandle(q);
+      for (int k = 0; k < p.coef_chunks; k++)
+        if (p.coef[k]) (void)hipIpcCloseMemHandle(p.coef[k]);
     }
     p = cairo_ctx::Peer();
   }
@@ -313,7 +352,9 @@ void free_ctx(cairo_ctx* c) {
   if (c->ps) (void)hipStreamDestroy(c->ps);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
   leave_group(c);
-  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->coef, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress, (void*)c->feed_dev, (void*)c->feed_hdr, (void*)c->feed_scratch,
+  for (int16_t* q : c->coef)
+    if (q) (void)hipFree(q);
+  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress, (void*)c->feed_dev, (void*)c->feed_hdr, (void*)c->feed_scratch,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps})
     (void)hipFree(p);
@@ -332,7 +373,9 @@ void free_ctx(cairo_ctx* c) {
 int zero_state(cairo_ctx* c) {
   const size_t S = (size_t)c->stages;
   CK(hipMemsetAsync(c->src, 0, c->plane_elems * 2 * S, c->ks));
-  CK(hipMemsetAsync(c->coef, 0, c->plane_elems * 2 * S, c->ks));
+  for (int k = 0; k < c->coef_chunks; k++)
+    CK(hipMemsetAsync(c->coef[k], 0, c->plane_elems * 2 * (size_t)std::min(c->coef_per, c->stages - k * c->coef_per),
+                      c->ks));
   CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
   CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * S, c->ks));
   // inter records: a frame whose search was cut short by a timed-out wait
@@ -448,8 +491,7 @@ int flush(cairo_ctx* c) {
     if (f.decode) {
       CK(hipMemcpyAsync(c->table + (size_t)f.slot * c->mbs, f.host_table, c->mbs * sizeof(BlockDesc),
                         hipMemcpyHostToDevice, st));
-      CK(hipMemcpyAsync(c->coef + (size_t)f.slot * c->plane_elems, f.host_coef, c->plane_elems * 2,
-                        hipMemcpyHostToDevice, st));
+      CK(hipMemcpyAsync(coef_base(c, f.slot), f.host_coef, c->plane_elems * 2, hipMemcpyHostToDevice, st));
     }
   }
   CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, st));
@@ -523,8 +565,7 @@ int flush(cairo_ctx* c) {
     CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
                       hipMemcpyDeviceToHost, c->cs));
     if (c->outputs & CAIRO_OUT_COEF)
-      CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2,
-                        hipMemcpyDeviceToHost, c->cs));
+      CK(hipMemcpyAsync(s.coef, coef_base(c, slot), c->plane_elems * 2, hipMemcpyDeviceToHost, c->cs));
     CK(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
     CK(hipEventRecord(s.d2h_done, c->cs));
     s.launched = true;
@@ -558,10 +599,11 @@ void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
     for (int k = 0; k < kMaxRing; k++) f.recon[k] = k < R ? recon_of(n - k) : zero;
     f.stale = recon_of(n - R);
     f.progress = c->progress + (size_t)f.slot * c->hmb;
+    f.coef = coef_planes(c, f.slot);
     if (n >= 1) {
       const cairo_ctx::Peer& p = c->gp[(n - 1) % N];
       const int ps = (int)(((n - 1) / N) % p.stages);
-      f.coef_prev = slot_planes(p.coef, c, ps);
+      f.coef_prev = peer_coef_planes(p, c, ps);
       f.prev_progress = p.progress + (size_t)ps * c->hmb;
     } else {
       f.coef_prev = zero;
@@ -581,7 +623,8 @@ void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
     f.recon[k] = slot_planes(c->ring_buf, c, k < R ? (int)(((uint32_t)f.index + R - k) % R) : 0);
   f.stale = f.recon[0];
   const int ps = (t + c->stages - 1) % c->stages;
-  f.coef_prev = slot_planes(c->coef, c, ps);
+  f.coef = coef_planes(c, f.slot);
+  f.coef_prev = coef_planes(c, ps);
   f.progress = c->progress + (size_t)f.slot * c->hmb;
   f.prev_progress = c->fresh ? nullptr : c->progress + (size_t)ps * c->hmb;
   f.prev2_progress = c->since_fresh < 2 ? nullptr : c->progress + (size_t)((t + 2 * c->stages - 2) % c->stages) * c->hmb;
@@ -660,7 +703,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
   const size_t S = (size_t)stages;
   TRY(hipMalloc(&c->src, c->plane_elems * 2 * S));
-  TRY(hipMalloc(&c->coef, c->plane_elems * 2 * S));
+  TRY(alloc_coef(c, false, c->coef, &c->coef_chunks, &c->coef_per));
   TRY(hipMalloc(&c->ring_buf, c->plane_elems * 2 * ring));
   TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * S));
   TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * S));
@@ -1055,8 +1098,7 @@ int cairo_ctx_fetch_coef(cairo_ctx* c, int ticket, cairo_frame_result* out) {
       std::lock_guard<std::mutex> lk(c->mu);
       if (!c->fs) CK(hipStreamCreateWithFlags(&c->fs, hipStreamNonBlocking));  // rare: made on first use
     }
-    CK(hipMemcpyAsync(s.coef, c->coef + (size_t)slot * c->plane_elems, c->plane_elems * 2, hipMemcpyDeviceToHost,
-                      c->fs));
+    CK(hipMemcpyAsync(s.coef, coef_base(c, slot), c->plane_elems * 2, hipMemcpyDeviceToHost, c->fs));
     CK(hipStreamSynchronize(c->fs));
   }
   out->coef_y = s.coef;
@@ -1077,34 +1119,35 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->fresh || c->npend || c->gsize > 1) return kInvalidResource;  // before any frame, outside a group
   CK(hipSetDevice(c->device));
-  // Importing an IPC buffer of 2 GiB or more never returned on the test
-  // boxes (a 4K context with 96 staging slots exports 2.4 GB of
-  // output_cache): refuse instead; a group member needs few staging slots.
-  if (cross_device && c->plane_elems * 2 * (size_t)c->stages >= (size_t(1) << 31)) {
-    fprintf(stderr, "[cairo_amd] peer_info: %d staging slots export %.2f GB of output_cache; IPC imports need < 2 GiB "
-                    "(create the member with fewer stages)\n", c->stages, c->plane_elems * 2.0 * c->stages / 1e9);
-    return kInvalidArg;
-  }
   if (cross_device && !c->fine_grained) {
     // Memory another device reads while this one writes it: fine-grained, so
     // that system-scope releases and acquires order it across devices.
     const size_t S = (size_t)c->stages;
-    int16_t *ring = nullptr, *coef = nullptr;
+    int16_t* ring = nullptr;
+    int16_t* coef[CAIRO_MAX_COEF_CHUNKS] = {};
+    int chunks = 0, per = 0;
     uint64_t* prog = nullptr;
     hipError_t e = hipExtMallocWithFlags((void**)&ring, c->plane_elems * 2 * c->ring, hipDeviceMallocFinegrained);
-    if (e == hipSuccess) e = hipExtMallocWithFlags((void**)&coef, c->plane_elems * 2 * S, hipDeviceMallocFinegrained);
+    if (e == hipSuccess) e = alloc_coef(c, true, coef, &chunks, &per);
     if (e == hipSuccess)
       e = hipExtMallocWithFlags((void**)&prog, (size_t)c->hmb * sizeof(uint64_t) * S, hipDeviceMallocFinegrained);
     if (e != hipSuccess) {
-      for (void* q : {(void*)ring, (void*)coef, (void*)prog}) (void)hipFree(q);
+      for (void* q : {(void*)ring, (void*)prog}) (void)hipFree(q);
+      for (int16_t* q : coef)
+        if (q) (void)hipFree(q);
       return fail(e, "hipExtMallocWithFlags(fine-grained)");
     }
     int r0 = sync_all(c);  // nothing is in flight (fresh), but the zeroing memsets may be
     if (r0) return r0;
     (void)hipFree(c->ring_buf);
-    (void)hipFree(c->coef);
+    for (int16_t*& q : c->coef) {
+      if (q) (void)hipFree(q);
+      q = nullptr;
+    }
     (void)hipFree(c->progress);
-    c->ring_buf = ring, c->coef = coef, c->progress = prog;
+    c->ring_buf = ring, c->progress = prog;
+    for (int k = 0; k < CAIRO_MAX_COEF_CHUNKS; k++) c->coef[k] = coef[k];
+    c->coef_chunks = chunks, c->coef_per = per;
     c->fine_grained = true;
     int r = zero_state(c);
     if (r) return r;
@@ -1115,18 +1158,25 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
   out->pid = (int32_t)getpid();
   out->stages = c->stages;
   out->fine_grained = c->fine_grained;
+  out->coef_chunks = c->coef_chunks;
+  out->coef_chunk_slots = c->coef_per;
   out->ring_addr = (uint64_t)(uintptr_t)c->ring_buf;
-  out->coef_addr = (uint64_t)(uintptr_t)c->coef;
   out->progress_addr = (uint64_t)(uintptr_t)c->progress;
-  void* bufs[3] = {c->ring_buf, c->coef, c->progress};
-  for (int k = 0; k < 3; k++) {
-    hipIpcMemHandle_t h;
-    CK(hipIpcGetMemHandle(&h, bufs[k]));
-    static_assert(sizeof(h) == sizeof(out->ipc[0]), "IPC handle size");
-    memcpy(out->ipc[k], &h, sizeof(h));
+  hipIpcMemHandle_t h;
+  static_assert(sizeof(h) == sizeof(out->ipc_ring), "IPC handle size");
+  CK(hipIpcGetMemHandle(&h, c->ring_buf));
+  memcpy(out->ipc_ring, &h, sizeof(h));
+  CK(hipIpcGetMemHandle(&h, c->progress));
+  memcpy(out->ipc_progress, &h, sizeof(h));
+  for (int k = 0; k < c->coef_chunks; k++) {
+    out->coef_addr[k] = (uint64_t)(uintptr_t)c->coef[k];
+    CK(hipIpcGetMemHandle(&h, c->coef[k]));
+    memcpy(out->ipc_coef[k], &h, sizeof(h));
   }
   return kSuccess;
 }
+
+int cairo_peer_size(void) { return (int)sizeof(cairo_peer); }
 
 int cairo_group_check_queues(int local_members) {
   // Members in one process on one device share that process's hardware
@@ -1177,8 +1227,19 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
     const cairo_peer& p = peers[i];
     q.stages = p.stages;
     if (i == rank) {
-      q.ring = c->ring_buf, q.coef = c->coef, q.progress = c->progress;
-    } else if (p.pid == me) {  // same process: the addresses are valid here
+      q.ring = c->ring_buf, q.progress = c->progress;
+      for (int k = 0; k < CAIRO_MAX_COEF_CHUNKS; k++) q.coef[k] = c->coef[k];
+      q.coef_chunks = c->coef_chunks, q.coef_per = c->coef_per;
+      continue;
+    }
+    if (p.coef_chunks < 1 || p.coef_chunks > CAIRO_MAX_COEF_CHUNKS || p.coef_chunk_slots < 1 ||
+        (long)p.coef_chunks * p.coef_chunk_slots < p.stages) {
+      c->gsize = i;
+      leave_group(c);
+      return kInvalidArg;
+    }
+    q.coef_chunks = p.coef_chunks, q.coef_per = p.coef_chunk_slots;
+    if (p.pid == me) {  // same process: the addresses are valid here
       if (p.device != c->device) {
         const hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
@@ -1188,23 +1249,23 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
         }
       }
       q.ring = (int16_t*)(uintptr_t)p.ring_addr;
-      q.coef = (int16_t*)(uintptr_t)p.coef_addr;
       q.progress = (uint64_t*)(uintptr_t)p.progress_addr;
-    } else {  // another process: open its IPC handles (peer access over xGMI)
-      void* m[3] = {nullptr, nullptr, nullptr};
-      for (int k = 0; k < 3; k++) {
+      for (int k = 0; k < p.coef_chunks; k++) q.coef[k] = (int16_t*)(uintptr_t)p.coef_addr[k];
+    } else {  // another process: open its IPC handles (peer access over xGMI), each allocation < 1 GiB
+      q.imported = true;  // leave_group closes whatever is open
+      auto open = [&](const uint8_t* bytes, void** dst) {
         hipIpcMemHandle_t h;
-        memcpy(&h, p.ipc[k], sizeof(h));
-        const hipError_t e = hipIpcOpenMemHandle(&m[k], h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) {
-          for (int j = 0; j < k; j++) (void)hipIpcCloseMemHandle(m[j]);
-          c->gsize = i;
-          leave_group(c);
-          return fail(e, "hipIpcOpenMemHandle");
-        }
+        memcpy(&h, bytes, sizeof(h));
+        return hipIpcOpenMemHandle(dst, h, hipIpcMemLazyEnablePeerAccess);
+      };
+      hipError_t e = open(p.ipc_ring, (void**)&q.ring);
+      if (e == hipSuccess) e = open(p.ipc_progress, (void**)&q.progress);
+      for (int k = 0; e == hipSuccess && k < p.coef_chunks; k++) e = open(p.ipc_coef[k], (void**)&q.coef[k]);
+      if (e != hipSuccess) {
+        c->gsize = i + 1;
+        leave_group(c);
+        return fail(e, "hipIpcOpenMemHandle");
       }
-      q.ring = (int16_t*)m[0], q.coef = (int16_t*)m[1], q.progress = (uint64_t*)m[2];
-      q.imported = true;
     }
   }
   c->gsize = size;
@@ -1247,7 +1308,7 @@ int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16
   if (r) return r;
   if (which < 2 && c->last_slot < 0) return kInvalidResource;
   PlaneSet p = which == 0 ? slot_planes(c->src, c, c->last_slot)
-               : which == 1 ? slot_planes(c->coef, c, c->last_slot)
+               : which == 1 ? coef_planes(c, c->last_slot)
                             : slot_planes(c->ring_buf, c, which - 2);
   const size_t ly = (size_t)c->wa * c->ha, lc = ly / 4;
   if (y) CK(hipMemcpy(y, p.y, ly * 2, hipMemcpyDeviceToHost));

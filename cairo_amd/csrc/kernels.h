@@ -71,6 +71,7 @@ struct FrameDesc {
   // FrameArgs):
   PlaneSet recon[kMaxRing];  // [0] this frame's reconstruction, [off] the reference at offset off
   PlaneSet stale;            // frame index-R's deblocked output (the rows below the intra search)
+  PlaneSet coef;             // this frame's output_cache (its staging slot's)
   PlaneSet coef_prev;        // the previous frame's output_cache (copy-macroblock chain)
   uint64_t* progress;        // this frame's deblock progress words [hmb]
   const uint64_t* prev_progress;  // the previous frame's (nullptr: none, first frame after a reset)
@@ -157,7 +158,6 @@ struct EngineArgs {
   const FrameArgs* fa;     // [nframes] per-frame views, device memory
   // per-slot buffers: base + slot * stride
   int16_t* src_base;    // plane sets, stride plane_elems
-  int16_t* coef_base;   // plane sets, stride plane_elems
   size_t plane_elems;
   BlockDesc* table_base;   // stride mbs
   BlockDesc* idesc_base;   // stride nref * mbs

@@ -2094,7 +2094,7 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.quality = f.quality;
   a.epoch = f.epoch;
   a.in = ring_slot(e.src_base, e.plane_elems, e.wa, e.ha, f.slot);
-  a.coef = ring_slot(e.coef_base, e.plane_elems, e.wa, e.ha, f.slot);
+  a.coef = f.coef;
   a.coef_prev = f.coef_prev;
   for (int k = 0; k < kMaxRing; k++) a.recon[k] = f.recon[k];
   a.stale = f.stale;

@@ -175,14 +175,24 @@ CAIRO_API int cairo_ctx_set_workgroups(cairo_ctx *ctx, int mb_rows);
  * one device share its workgroup slots: give each cairo_ctx_max_workgroups /
  * (members on the device) row coders (cairo_ctx_set_workgroups).
  * cairo_ctx_reset leaves the group. */
+#define CAIRO_MAX_COEF_CHUNKS 16
 typedef struct cairo_peer {
   uint32_t width, height, ring;
-  int32_t device, pid, stages, fine_grained, reserved;
-  uint64_t ring_addr, coef_addr, progress_addr; /* device addresses in the owner's process */
-  uint8_t ipc[3][64];                           /* hipIpcMemHandle_t of the three buffers */
+  int32_t device, pid, stages, fine_grained;
+  int32_t coef_chunks;      /* the output_cache slots live in this many allocations */
+  int32_t coef_chunk_slots; /* staging slots per chunk: slot s is in chunk s / coef_chunk_slots */
+  int32_t reserved;
+  uint64_t ring_addr, progress_addr;             /* device addresses in the owner's process */
+  uint64_t coef_addr[CAIRO_MAX_COEF_CHUNKS];
+  uint8_t ipc_ring[64], ipc_progress[64];        /* hipIpcMemHandle_t of each allocation */
+  uint8_t ipc_coef[CAIRO_MAX_COEF_CHUNKS][64];
 } cairo_peer;
-/* (A member's exported output_cache, 2 bytes x 1.5 x Wa x Ha x stages, must
- * stay below 2 GiB: larger IPC imports did not return on the test boxes.) */
+/* A member's output_cache (2 bytes x 1.5 x Wa x Ha per staging slot) is
+ * allocated in chunks of at most 1 GiB, each exported with its own IPC handle:
+ * an IPC import of a single fine-grained allocation of 2 GiB or more never
+ * returned on the test boxes (a 4K member with 96 slots has 2.4 GB of it). */
+/* sizeof(cairo_peer), for bindings that exchange the records as bytes. */
+CAIRO_API int cairo_peer_size(void);
 CAIRO_API int cairo_ctx_peer_info(cairo_ctx *ctx, int cross_device, cairo_peer *out);
 CAIRO_API int cairo_ctx_join_group(cairo_ctx *ctx, int size, int rank, const cairo_peer *peers);
 /* Whether local_members group members may share one process and device:

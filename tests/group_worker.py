@@ -101,13 +101,16 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo", init_method=f"file://{a.store}", rank=a.rank, world_size=N)
-        ctx = cairo_amd.Context(w, h, ring)
+        ctx = cairo_amd.Context(w, h, ring)  # the library's default staging slots (96)
         ctx.set_batch(a.batch)
         if a.feed:
             ctx.set_outputs(cairo_amd.OUT_FEED)
         ctx.set_workgroups(max(1, ctx.max_workgroups() // N))  # N members share the device
         recs = [None] * N
-        dist.all_gather_object(recs, ctx.peer_info(cross_device=True))
+        rec = ctx.peer_info(cross_device=True)
+        if ctx.stages * ctx.wa * ctx.ha * 3 >= 1 << 31:  # the export is chunked below 1 GiB per allocation
+            assert int.from_bytes(rec[28:32], "little") >= 2, "output_cache exported in one allocation"
+        dist.all_gather_object(recs, rec)
         ctx.join_group(a.rank, recs)
         mine = [t for t in range(F) if t % N == a.rank]
         frames = {t: orc.make_frame(w, h, t) for t in mine}

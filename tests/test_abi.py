@@ -88,3 +88,9 @@ def test_group_queue_check(cairo, monkeypatch):
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "32")
     assert L.cairo_group_check_queues(10) == 0
     assert L.cairo_group_check_queues(11) == 1  # 35 queues: more than HIP allows
+
+
+def test_peer_record_size(cairo):
+    """The Python binding exchanges cairo_peer records as bytes: its size
+    matches the library's (chunked output_cache handles, include/cairo_amd.h)."""
+    assert cairo.lib().cairo_peer_size() == cairo.PEER_SIZE

@@ -64,8 +64,9 @@ def test_group_4k_in_process():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("members,feed,frames", [(2, False, 12), (2, True, 12), (3, True, 12)])
-def test_group_cross_process(tmp_path, members, feed, frames):
+@pytest.mark.parametrize("members,feed,frames,size", [(2, False, 12, "cif"), (2, True, 12, "cif"), (3, True, 12, "cif"),
+                                                      (2, True, 6, "4k")])
+def test_group_cross_process(tmp_path, members, feed, frames, size):
     """One process per member on one device: buffers shared through IPC
     handles (fine-grained memory, system-scope hand-offs: the cross-GPU code
     path), records exchanged over gloo; with feed, the members hand over
@@ -73,13 +74,15 @@ def test_group_cross_process(tmp_path, members, feed, frames):
     frame's payload is checked against the oracle's."""
     store = tmp_path / "store"
     extra = ["--feed"] if feed else []
+    if size == "4k":  # BASELINE configs[3] geometry with the library's 96 staging slots: 2.4 GB of
+        extra += ["--w", "3840", "--h", "2160"]  # output_cache per member, imported in two chunks
     procs = [subprocess.Popen([sys.executable, WORKER, "xproc", "--members", str(members), "--rank", str(k), "--store",
                                str(store), "--frames", str(frames), "--batch", "3"] + extra, cwd=ROOT,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for k in range(members)]
     outs = []
     for p in procs:
         try:
-            o, e = p.communicate(timeout=240)
+            o, e = p.communicate(timeout=280)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
