@@ -400,15 +400,29 @@ class Context:
         _ck(self.L.cairo_ctx_join_group(self.h, len(peers), rank, arr), "cairo_ctx_join_group")
 
 
-def group_layout(n: int, size: int, ring: int, stages: int) -> dict:
+MIRROR_SLOTS = 16  # kMirrorSlots (backend.hip): reconstruction slots of a member over devices / processes
+
+
+def group_layout(n: int, size: int, ring: int, stages: int, mirror: bool = False) -> dict:
     """Where frame n of a frame-interleaved group of `size` members lives
     (backend.hip frame_links): its member, that member's ticket, staging
     slot and reconstruction slot, and whether it reconstructs in place over
-    frame n - ring (the reference's ring reuse, common.cpp:192-195)."""
-    slots = -(-ring // size)  # ceil(R / N) reconstruction slots per member
+    frame n - ring (the reference's ring reuse, common.cpp:192-195).  mirror:
+    members on other devices or processes, whose rings all share one layout
+    (slot (n % N) * S + (n / N) % S: the producer's own block, a mirror block
+    on every other member); `readers` are the members its deblock pushes it
+    to (the frames n+1..n+R-1 reference it, n+R reads its stale rows)."""
+    slots = -(-ring // size)  # S = ceil(R / N) reconstruction slots per member (per block when mirrored)
     t = n // size
-    return {"member": n % size, "ticket": t, "staging_slot": t % stages, "recon_slot": t % slots,
-            "recon_slots": slots, "in_place": size * slots == ring}
+    slot = (n % size) * slots + t % slots if mirror else t % slots
+    readers = []
+    if mirror:
+        for d in range(1, ring + 1):
+            j = (n + d) % size
+            if j != n % size and j not in readers:
+                readers.append(j)
+    return {"member": n % size, "ticket": t, "staging_slot": t % stages, "recon_slot": slot,
+            "recon_slots": slots * size if mirror else slots, "in_place": size * slots == ring, "readers": readers}
 
 
 class Group:
@@ -461,7 +475,7 @@ class Group:
 
     def recon(self, n: int):
         """Frame n's deblocked reconstruction (y, u, v), while still held."""
-        lay = group_layout(n, self.size, self.ring, self.stages)
+        lay = group_layout(n, self.size, self.ring, self.stages, mirror=self.cross)
         return self.members[lay["member"]].read_planes(2 + lay["recon_slot"])
 
     def close(self) -> None:

@@ -59,6 +59,11 @@ constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads i
 // exported with its own IPC handle (cairo_peer): an IPC import of one
 // fine-grained allocation of 2 GiB or more never returned.
 constexpr size_t kCoefChunkBytes = size_t(1) << 30;
+// Reconstruction slots of a member of a group over several devices or
+// processes: every member keeps the same layout, N * S slots (S = ceil(R / N)),
+// frame m in slot (m % N) * S + (m / N) % S -- its producer's own block, a
+// mirror block on every other member -- for any N <= kMaxGroup.
+constexpr int kMirrorSlots = kMaxGroup > kMaxRing ? kMaxGroup : kMaxRing;
 constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5,  // evx_status (base.h:150-172)
               kInvalidResource = 8;
 
@@ -131,6 +136,7 @@ struct cairo_ctx {
   uint64_t* gran = nullptr;
   uint8_t* rgb = nullptr;
   int16_t* ring_buf = nullptr;
+  int ring_slots = 0;  // R; kMirrorSlots once allocated for a group over devices / processes
   uint64_t* progress = nullptr;  // [stages][hmb] tagged deblock progress of each slot's frame
   bool fresh = true;             // no frame since create / reset: the next has no predecessor
   long since_fresh = 0;          // frames since create / reset (frame_links)
@@ -376,7 +382,7 @@ int zero_state(cairo_ctx* c) {
   for (int k = 0; k < c->coef_chunks; k++)
     CK(hipMemsetAsync(c->coef[k], 0, c->plane_elems * 2 * (size_t)std::min(c->coef_per, c->stages - k * c->coef_per),
                       c->ks));
-  CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring, c->ks));
+  CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring_slots, c->ks));
   CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * S, c->ks));
   // inter records: a frame whose search was cut short by a timed-out wait
   // still reads in-frame motion vectors
@@ -591,13 +597,29 @@ void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
     const int N = c->gsize, S = (R + N - 1) / N;
     const long n = f.index;
     const PlaneSet zero = planes_at(c->zero, c);
+    // Members on other devices or processes (sys) keep mirrors: every frame
+    // read here is local (slot (m % N) * S + (m / N) % S of this member's
+    // ring), and this frame's deblock pushes it into the same slot of each
+    // member that reads it.  Members on one device read each other's rings.
+    const bool mirror = c->sys && c->fine_grained && c->ring_slots >= N * S;
+    auto slot_of = [&](long m) { return mirror ? (int)((m % N) * S + (m / N) % S) : (int)((m / N) % S); };
     auto recon_of = [&](long m) {
       if (m < 0) return zero;
-      const cairo_ctx::Peer& p = c->gp[m % N];
-      return slot_planes(p.ring, c, (int)((m / N) % S));
+      return slot_planes(mirror ? c->ring_buf : c->gp[m % N].ring, c, slot_of(m));
     };
     for (int k = 0; k < kMaxRing; k++) f.recon[k] = k < R ? recon_of(n - k) : zero;
     f.stale = recon_of(n - R);
+    f.npush = 0;
+    if (mirror) {
+      bool seen[kMaxGroup] = {};
+      seen[c->grank] = true;
+      for (int d = 1; d <= R; d++) {  // the frames n+1..n+R-1 reference it, n+R reads its stale rows
+        const int j = (int)((n + d) % N);
+        if (seen[j]) continue;
+        seen[j] = true;
+        f.push[f.npush++] = slot_planes(c->gp[j].ring, c, slot_of(n));
+      }
+    }
     f.progress = c->progress + (size_t)f.slot * c->hmb;
     f.coef = coef_planes(c, f.slot);
     if (n >= 1) {
@@ -621,6 +643,7 @@ void frame_links(cairo_ctx* c, FrameDesc& f, int t) {
   }
   for (int k = 0; k < kMaxRing; k++)
     f.recon[k] = slot_planes(c->ring_buf, c, k < R ? (int)(((uint32_t)f.index + R - k) % R) : 0);
+  f.npush = 0;
   f.stale = f.recon[0];
   const int ps = (t + c->stages - 1) % c->stages;
   f.coef = coef_planes(c, f.slot);
@@ -705,6 +728,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipMalloc(&c->src, c->plane_elems * 2 * S));
   TRY(alloc_coef(c, false, c->coef, &c->coef_chunks, &c->coef_per));
   TRY(hipMalloc(&c->ring_buf, c->plane_elems * 2 * ring));
+  c->ring_slots = (int)ring;
   TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * S));
   TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * S));
   TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * S));
@@ -1127,7 +1151,7 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
     int16_t* coef[CAIRO_MAX_COEF_CHUNKS] = {};
     int chunks = 0, per = 0;
     uint64_t* prog = nullptr;
-    hipError_t e = hipExtMallocWithFlags((void**)&ring, c->plane_elems * 2 * c->ring, hipDeviceMallocFinegrained);
+    hipError_t e = hipExtMallocWithFlags((void**)&ring, c->plane_elems * 2 * kMirrorSlots, hipDeviceMallocFinegrained);
     if (e == hipSuccess) e = alloc_coef(c, true, coef, &chunks, &per);
     if (e == hipSuccess)
       e = hipExtMallocWithFlags((void**)&prog, (size_t)c->hmb * sizeof(uint64_t) * S, hipDeviceMallocFinegrained);
@@ -1146,6 +1170,7 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
     }
     (void)hipFree(c->progress);
     c->ring_buf = ring, c->progress = prog;
+    c->ring_slots = kMirrorSlots;
     for (int k = 0; k < CAIRO_MAX_COEF_CHUNKS; k++) c->coef[k] = coef[k];
     c->coef_chunks = chunks, c->coef_per = per;
     c->fine_grained = true;
@@ -1301,7 +1326,7 @@ int cairo_ctx_sync(cairo_ctx* c) {
 }
 
 int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16_t* v) {
-  if (!c || which < 0 || which >= 2 + (int)c->ring) return kInvalidArg;
+  if (!c || which < 0 || which >= 2 + c->ring_slots) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
   int r = sync_all(c);

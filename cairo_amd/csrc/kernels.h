@@ -55,6 +55,9 @@ __host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
 constexpr int kMaxBatch = CAIRO_MAX_BATCH;
 // Members of a frame-interleaved group (cairo_ctx_join_group).
 constexpr int kMaxGroup = 16;
+// Members a frame's reconstruction is pushed to (its R-1 referencing frames
+// and the stale-row reader R frames later live on at most R other members).
+constexpr int kMaxPush = kMaxRing;
 
 // One frame of a batch (host-filled, kernarg).
 struct FrameDesc {
@@ -72,6 +75,8 @@ struct FrameDesc {
   PlaneSet recon[kMaxRing];  // [0] this frame's reconstruction, [off] the reference at offset off
   PlaneSet stale;            // frame index-R's deblocked output (the rows below the intra search)
   PlaneSet coef;             // this frame's output_cache (its staging slot's)
+  PlaneSet push[kMaxPush];   // FrameArgs::push
+  int npush;
   PlaneSet coef_prev;        // the previous frame's output_cache (copy-macroblock chain)
   uint64_t* progress;        // this frame's deblock progress words [hmb]
   const uint64_t* prev_progress;  // the previous frame's (nullptr: none, first frame after a reset)
@@ -104,6 +109,12 @@ struct FrameArgs {
   // for the first R frames).  The reference reuses that slot in place, so this
   // equals recon[0] whenever the group's slot arithmetic does too.
   PlaneSet stale;
+  // Mirrors of recon[0] on the members that read this frame (a group on
+  // several devices or processes): the deblock stores every written word to
+  // each of them as well, before the progress word that declares it final,
+  // so the readers' searches read local memory instead of a peer's over xGMI.
+  PlaneSet push[kMaxPush];
+  int npush;
   BlockDesc* table;    // [wmb*hmb]
   BlockDesc* inter_desc;  // [(off-1)*mbs + mb]
   int32_t* inter_sad;     // [(off-1)*mbs + mb]

@@ -1255,6 +1255,10 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
         const uint32_t d = (uint32_t)(uint16_t)p[0] | ((uint32_t)(uint16_t)p[1] << 16);
         __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)g, d, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        const size_t off = (size_t)(g - pick(cs, pl));
+        for (int q = 0; q < a.npush; q++)  // the readers' mirrors (uniform loop)
+          __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(pick(planes(a.push[q]), pl) + off), d,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -2111,6 +2115,8 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.progress = f.progress;
   a.prev_progress = f.prev_progress;
   a.prev2_progress = f.prev2_progress;
+  a.npush = f.npush;
+  for (int k = 0; k < kMaxPush; k++) a.push[k] = f.push[k];
   a.sys = f.sys;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   {

@@ -127,12 +127,12 @@ def main():
             elif any(not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
                 bad.append(t)
             ctx.release(tk[t])
-        S = -(-ring // N)
-        for t, planes in final.items():
-            if t % N == a.rank:
-                got = ctx.read_planes(2 + (t // N) % S)
+        for t, planes in final.items():  # its own frames, and the mirrors other members pushed here
+            lay = cairo_amd.group_layout(t, N, ring, ctx.stages, mirror=True)
+            if lay["member"] == a.rank or a.rank in lay["readers"]:
+                got = ctx.read_planes(2 + lay["recon_slot"])
                 if any(not np.array_equal(x, y) for x, y in zip(got, planes)):
-                    bad.append(f"recon {t}")
+                    bad.append(f"recon {t}" + ("" if lay["member"] == a.rank else " (mirror)"))
         dist.barrier()  # the others may still read this member's buffers until they finish
         ctx.close()
         dist.destroy_process_group()

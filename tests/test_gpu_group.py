@@ -65,13 +65,15 @@ def test_group_4k_in_process():
 
 
 @pytest.mark.parametrize("members,feed,frames,size", [(2, False, 12, "cif"), (2, True, 12, "cif"), (3, True, 12, "cif"),
-                                                      (2, True, 6, "4k")])
+                                                      (4, True, 16, "cif"), (8, True, 20, "cif"), (2, True, 6, "4k")])
 def test_group_cross_process(tmp_path, members, feed, frames, size):
     """One process per member on one device: buffers shared through IPC
     handles (fine-grained memory, system-scope hand-offs: the cross-GPU code
-    path), records exchanged over gloo; with feed, the members hand over
-    GPU-precoded feeds as bench.py's single-stream leg does, and every
-    frame's payload is checked against the oracle's."""
+    path, each frame's deblock pushing it into the mirrors of the members
+    that read it), records exchanged over gloo; with feed, the members hand
+    over GPU-precoded feeds as bench.py's single-stream leg does, and every
+    frame's payload is checked against the oracle's.  8 members: the node's
+    GPU count (every frame pushed to R = 4 other members)."""
     store = tmp_path / "store"
     extra = ["--feed"] if feed else []
     if size == "4k":  # BASELINE configs[3] geometry with the library's 96 staging slots: 2.4 GB of

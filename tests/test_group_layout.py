@@ -43,6 +43,34 @@ def test_layout_invariants(size, ring):
         seen[key] = n
 
 
+@pytest.mark.parametrize("size", [2, 3, 4, 5, 8, 16])
+@pytest.mark.parametrize("ring", [2, 3, 4])
+def test_mirror_layout(size, ring):
+    """Members on other devices / processes keep every frame they read in a
+    local mirror slot (backend.hip frame_links, mirror mode): the slots fit
+    the ring every member allocates, a slot is rewritten only by the same
+    producer's frame N * S >= R later, and each frame is pushed to exactly the
+    other members holding its R-1 referencing frames and its stale-row reader."""
+    frames = 200
+    lay = [cairo_amd.group_layout(n, size, ring, 8, mirror=True) for n in range(frames)]
+    S = -(-ring // size)
+    assert size * S <= cairo_amd.MIRROR_SLOTS
+    holder = {}
+    for n in range(frames):
+        slot = lay[n]["recon_slot"]
+        assert slot // S == n % size  # the producer's block
+        if slot in holder:
+            assert n - holder[slot] == size * S >= ring
+        holder[slot] = n
+        want = {(n + d) % size for d in range(1, ring + 1)} - {n % size}
+        assert set(lay[n]["readers"]) == want and len(lay[n]["readers"]) <= 4
+        # every frame n reads (n-1..n-R) is local: produced here or pushed here
+        for d in range(1, ring + 1):
+            if n - d >= 0:
+                src = lay[n - d]
+                assert src["member"] == n % size or n % size in src["readers"]
+
+
 def _rank(rank, world, store, out):
     dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     rec = bytes([rank]) * cairo_amd.PEER_SIZE  # stands in for Context.peer_info()
