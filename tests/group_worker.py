@@ -127,6 +127,8 @@ def main():
             elif any(not np.array_equal(x, y) for x, y in zip((out.coef_y, out.coef_u, out.coef_v), ref[t][2])):
                 bad.append(t)
             ctx.release(tk[t])
+        ctx.sync()
+        dist.barrier()  # every member's frames encoded: their pushes into this member's mirrors are done
         for t, planes in final.items():  # its own frames, and the mirrors other members pushed here
             lay = cairo_amd.group_layout(t, N, ring, ctx.stages, mirror=True)
             if lay["member"] == a.rank or a.rank in lay["readers"]:
