@@ -741,8 +741,11 @@ __device__ __forceinline__ int inter_need_cols(FA& a, int g, int level) {
   return min(64 * g + (level == 1 ? 80 : 96), a.wa);
 }
 
+// publish = 0: the task's records stay in flight (a later task of the group
+// drains them); publish = n: drain this wave's stores and add n to the group's
+// finished count (the coder waits for nref).
 __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLds& L, DbLds& D,
-                                           DbState& st, int* flag, uint64_t* is) {
+                                           DbState& st, int* flag, uint64_t* is, int publish) {
   const int wave = uni(threadIdx.x >> 6);  // scalar: the acceptance replay runs on SGPRs
   const int x = 4 * g + wave;
   const bool valid = x < a.wmb;
@@ -874,11 +877,19 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     __hip_atomic_store((gbl_u32*)&a.inter_sad[(off - 1) * mbs + mb], (uint32_t)s.sad, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
-  // all records of this task stored; release them to the row coder
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (publish) {
+    // all records of the group's tasks stored (vmcnt counts every store of
+    // the wave, earlier tasks' included); release them to the row coder
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    // the next task rewrites the window: every wave is done reading it (its
+    // LDS reads returned); the records' stores stay in flight (each one waits
+    // about 3.5 us for its write-through acknowledgement)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1911,14 +1922,14 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     // searches fill what used to be the wait for the previous frame.
     if (a.inter && a.nref >= 2) {
       helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
-      for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is);
+      for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is, 0);
     }
     // level 1 of the group's window in the previous frame; deblock meanwhile
     helper_wait(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
-      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is);
+      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is, a.nref);  // publishes the group's nref records
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
