@@ -815,23 +815,28 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
       // the wave-uniform results.  An out-of-frame candidate is evaluated at
       // the current best and not offered.
       if (si < 5) {
-        // Candidate c of the 3x3 in pass p (of 3) on lane group g: c = 4p + g
-        // (the last pass's groups 1..3 repeat candidate 8).  Lane c < 9 then
-        // collects candidate c (ds_bpermute from its group's first lane) and
-        // select_int replays the sequential acceptance on lanes 0..15.
+        // The 3x3's centre (candidate 4 in scan order) is the current best:
+        // its SAD and MAD are the state's (same position, same source), so only
+        // the 8 others are evaluated, in 2 passes of four 16-lane groups:
+        // pass p, group g -> candidate 4p + g, skipping 4.  Lane c < 9 then
+        // collects candidate c (ds_bpermute from its group's first lane; the
+        // centre from the state) and select_int replays the sequential
+        // acceptance on lanes 0..15 (the centre can still win there when an
+        // earlier candidate of the step was taken first).
         const int bx = s.bx, by = s.by;
         const int lane = threadIdx.x & 63, gi = lane & 15, grp = lane >> 4;
-        int sadv = 0, madv = 0;
+        const int my_pass = gi < 4 ? 0 : 1, my_grp = gi < 4 ? gi : gi - 5;  // where candidate gi is evaluated
+        int sadv = s.sad, madv = s.mad;  // lane 4: the centre
 #pragma unroll
-        for (int pass = 0; pass < 3; pass++) {
-          const int c = min(4 * pass + grp, 8);
+        for (int pass = 0; pass < 2; pass++) {
+          const int c = 4 * pass + grp + (pass > 0);  // 0..3, then 5..8
           const int cx = bx + (c % 3 - 1) * step, cy = by + (c / 3 - 1) * step;
           const bool ok = in_frame(cx, cy, a.wa, a.ha);
           int sad, mad;
           inter_cand_row(L.win, (ok ? cx : bx) - ox, (ok ? cy : by) - oy, gi, srow, sad, mad);
-          const int from = (16 * (lane & 3)) << 2;
+          const int from = (16 * (my_grp & 3)) << 2;
           const int vs = __builtin_amdgcn_ds_bpermute(from, sad), vm = __builtin_amdgcn_ds_bpermute(from, mad);
-          if ((gi >> 2) == pass) sadv = vs, madv = vm;
+          if (my_pass == pass && gi != 4) sadv = vs, madv = vm;
         }
         {
           const int cx = bx + (gi % 3 - 1) * step, cy = by + (gi / 3 - 1) * step;
