@@ -671,6 +671,13 @@ constexpr int kLvl1Rows = 77, kLvl1Cols = 112;
 #define CAIRO_HELPER_INTERLEAVE 1
 #endif
 constexpr bool kHelperInterleave = CAIRO_HELPER_INTERLEAVE;
+// The in-place deblock of a row is run by its row coder, in the waits for its
+// inter records (and at the end of the row), instead of by its helper: the
+// helpers' searches pace the rows, the coders wait for them.
+#ifndef CAIRO_CODER_DEBLOCK
+#define CAIRO_CODER_DEBLOCK 0
+#endif
+constexpr bool kCoderDeblock = CAIRO_CODER_DEBLOCK;
 
 // Thread 0's value v, broadcast to the workgroup (two barriers).
 __device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
@@ -703,7 +710,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
     if (threadIdx.x == 0) {
       if (!pp || progress_peer(a.sys, pp + rr) >= tagged(a.epoch - back, need)) {
         d = 1;
-      } else if (kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
+      } else if (!kCoderDeblock && kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
         d = 2;
       } else {  // nothing to do: back off
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -849,19 +856,42 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
         const int bx = s.bx, by = s.by;
         // accepted in the order they are evaluated (neighbour-major, half
         // then quarter), each as soon as its sums exist: no array of 16
-        // results stays live (it pushed the engine into scratch spills)
+        // results stays live (it pushed the engine into scratch spills).
+        // accept_sub (motion.cpp:151-223) needs the MAD only through
+        // "mad < limit" (copy mode: the best MAD, else thr), which is "no
+        // lane's maximum reaches limit": one ballot instead of a wave-wide
+        // max; the exact MAD (and, in copy mode, the SAD) is reduced only for
+        // an accepted candidate.
 #pragma unroll
         for (int n = 0; n < 8; n++) {
           const int k9 = n < 4 ? n : n + 1, i = k9 % 3 - 1, j = k9 / 3 - 1, tx = bx + i, ty = by + j;
           const bool ok = in_frame(tx, ty, a.wa, a.ha);
-          const Px6 nb = px_from_window(L.win, (ok ? tx : bx) - ox, (ok ? ty : by) - oy);
-          int cs[2], cm[2];
+          if (!ok) continue;  // (wave-uniform) out of frame: not offered
+          const Px6 nb = px_from_window(L.win, tx - ox, ty - oy);
+          const int idx = frac_index(i, j);
 #pragma unroll
-          for (int q = 0; q < 2; q++) sad_mad(src, lerp6(best, nb, q), cs[q], cm[q]);
-          if (ok) {
-            const int idx = frac_index(i, j);
-#pragma unroll
-            for (int q = 0; q < 2; q++) accept_sub(s, idx, q, cs[q], cm[q], thr);
+          for (int q = 0; q < 2; q++) {
+            const Px6 c = lerp6(best, nb, q);
+            const int d0 = abs(src.y0 - c.y0), d1 = abs(src.y1 - c.y1), d2 = abs(src.y2 - c.y2), d3 = abs(src.y3 - c.y3);
+            const int lsum = d0 + d1 + d2 + d3;
+            const int lmax = max(max(max(d0, d1), max(d2, d3)), max(abs(src.u - c.u), abs(src.v - c.v)));
+            const bool copy = s.mad < thr;
+            const bool mad_lt = __ballot(lmax >= (copy ? s.mad : thr)) == 0;
+            int sad = 0;
+            bool acc;
+            if (copy) {
+              acc = mad_lt;
+            } else {
+              sad = wave_sum(lsum);
+              acc = (sad < s.sad && sad < kSadGate) || mad_lt;
+            }
+            if (acc) {
+              s.sp_en = 1;
+              s.sp_amt = q;
+              s.sp_idx = idx;
+              s.sad = copy ? wave_sum(lsum) : sad;
+              s.mad = wave_max(lmax);
+            }
           }
         }
       }
@@ -1332,7 +1362,55 @@ struct alignas(16) RowLds {
   int16_t bufA[kMBElems], bufB[kMBElems];  // per-block transform scratch, block-major
   int32_t cand[2][16][2];                  // double-buffered candidate (sad, mad)
   int32_t red[12];
+#if CAIRO_CODER_DEBLOCK
+  DbLds db;  // the row's deblock tile
+#endif
 };
+
+// Deblock chunks the coder may leave pending at a group start before it runs
+// a ready one even when its inter records are already there (the next
+// frame's helpers wait for this row's progress).
+#ifndef CAIRO_CODER_DB_LAG
+#define CAIRO_CODER_DB_LAG 3
+#endif
+constexpr int kCoderDbLag = CAIRO_CODER_DB_LAG;
+
+// Row coder at the start of group g (MB bx = 4g): until the group's nref inter
+// records are in (inter_done), running this row's ready deblock chunks
+// meanwhile -- and a ready one anyway while more than kCoderDbLag chunks are
+// pending.  Only ready chunks run here (their inputs: this row's coded
+// macroblocks, the row above's progress), so the coder never blocks on a
+// deblock; bounded like every wait.
+template <int kDummy = 0>
+__device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbState& st, int* flag) {
+  volatile int* vflag = flag;
+  int32_t* word = &a.inter_done[by * a.ng + (bx >> 2)];
+  uint64_t t0 = 0;
+  for (;;) {
+    int d = 0;
+    if (threadIdx.x == 0) {
+      const bool recs = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.nref;
+      const bool can = st.k < bx && deblock_chunk_ready(a, by, st);
+      if (can && (!recs || bx - st.k > kCoderDbLag)) {
+        d = 2;
+      } else if (recs || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        d = 1;
+      } else {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (!t0) t0 = now;
+        __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
+        if (now - t0 > 200000000ull) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          d = 1;
+        }
+      }
+    }
+    d = wg_broadcast(vflag, d);
+    if (d == 1) break;
+    if (d == 2) deblock_chunk(a, by, D, st);
+  }
+}
 
 // Pixel pair (int16 lo = column col, hi = col+1; col even) of plane pl at
 // window row `row`.
@@ -1554,7 +1632,7 @@ __device__ __forceinline__ void coef_store_pair(FA& a, int e, int px, int py, in
 // kDecode: the decoder's reconstruction (decode_slice, decode.cpp:146-170) from
 // the given block table and coefficients, without the searches.
 template <bool kDecode>
-__device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) {
+__device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, int32_t* tr) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
@@ -1564,6 +1642,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
   const int mbs = a.wmb * a.hmb;
+#if CAIRO_CODER_DEBLOCK
+  DbState dst{0, 0, 0, 8};
+#endif
   {
     const int py = by * kMB, oy = py - 48;
     for (int bx = 0; bx < a.wmb; bx++) {
@@ -1573,7 +1654,11 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
       stamp(a, mb, 0);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
       if ((bx & 3) == 0) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
+#if CAIRO_CODER_DEBLOCK
+        coder_wait(a, by, bx, L.db, dst, flag);
+#else
         if (tid == 0) wait_at_least(&a.inter_done[by * a.ng + (bx >> 2)], a.nref, err, a.sticky);
+#endif
         acquire_after_wait(a.sys);  // the stale rows, references and previous output_cache
       }
 
@@ -1887,13 +1972,18 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int32_t* tr) 
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
   }
+#if CAIRO_CODER_DEBLOCK
+  // the rest of the row's deblock (each chunk waits for the row above)
+  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  while (dst.k < nch) deblock_chunk(a, by, L.db, dst);
+#endif
 }
 
 
 
 struct HelperLds {
   InterLds inter;
-  DbLds db;
+  DbLds db;  // (unused with the coder-side deblock)
 };
 
 struct EngineLds {
@@ -1941,15 +2031,15 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
       __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (is) is[2] = __builtin_amdgcn_s_memrealtime();
-    for (;;) {  // catch the deblock up with what has arrived
+    for (; !kCoderDeblock;) {  // catch the deblock up with what has arrived
       int d = 0;
-      if (tid == 0) d = kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
+      if (tid == 0) d = !kCoderDeblock && kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
       if (!wg_broadcast(vflag, d)) break;
       deblock_chunk(a, r, L.db, st);
     }
   }
   trace(tr, 1, 1000);
-  while (st.k < nch) {
+  while (!kCoderDeblock && st.k < nch) {
     trace(tr, 3, 60000 + st.k);
     deblock_chunk(a, r, L.db, st);
   }
@@ -2075,7 +2165,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
       if (t < 0) break;
       trace(e.trace, 0, 3000000 + t);
       const int32_t o = (prev ? e.porder : e.order)[t];
-      code_row<kDecode>(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.row, e.trace);
+      code_row<kDecode>(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.row, &L.flag, e.trace);
       task_done(prev ? e.psync : e.sync);
       trace(e.trace, 0, 4000000 + t);
     }
