@@ -739,6 +739,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
 struct InterLds {
   Window win;
   int need[4];
+  int full;  // the whole window is final (staged at once)
   int lvl2[6][4];  // per step (16, 8, 4, 2, 1, sub-pel) and wave: level 2 wanted
 };
 
@@ -775,14 +776,31 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   }
   const bool need = valid && s.mad >= thr;
   if ((threadIdx.x & 63) == 0) L.need[wave] = need;
+  if (threadIdx.x == 0) {
+    // Is the reference already final over the whole window (level 2 too)?
+    // Always, in practice, for the older references (frame index-2 runs far
+    // ahead): then the window is staged in one go and the steps skip the
+    // per-step level-2 decisions and their barriers.
+    const int back = off == 1 ? 1 : 2;
+    const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
+    const uint64_t want = tagged(a.epoch - back, inter_need_cols(a, g, 2));
+    const int full = !pp || (progress_peer(a.sys, pp + min(r + 3, a.hmb - 1)) >= want &&
+                             progress_peer(a.sys, pp + min(r + 2, a.hmb - 1)) >= want);
+    if (full && pp) {  // acquire what the progress words released (the loads below follow the barrier)
+      acquire_fence(a.sys);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    L.full = full;
+  }
   __syncthreads();
   if (is && off == 1) is[3] = __builtin_amdgcn_s_memrealtime();
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
     const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
-    load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, 0, kLvl1Cols);
+    const bool full = L.full != 0;  // workgroup-uniform
+    load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     __syncthreads();
     if (is && off == 1) is[4] = __builtin_amdgcn_s_memrealtime();
-    bool lvl2c = false, lvl2r = false;  // workgroup-uniform
+    bool lvl2c = full, lvl2r = full;  // workgroup-uniform
     bool lvl2_open = true;  // workgroup-uniform: some wave's search may still leave level 1
     // steps 16, 8, 4, 2, 1, then the sub-pel step (reach 1 around the best)
     for (int si = 0; si < 6; si++) {
