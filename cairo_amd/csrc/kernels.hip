@@ -1124,7 +1124,12 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 // stores and published as the row's progress.  Row r needs row r-1 one
 // macroblock ahead, while the row coders run two apart: the deblock keeps
 // up instead of drifting.
-constexpr int kDbChunk = 16;
+#ifndef CAIRO_DB_CHUNK
+#define CAIRO_DB_CHUNK 32
+#endif
+constexpr int kDbChunk = CAIRO_DB_CHUNK;  // luma columns per chunk: 16 or 32 (one or two macroblocks)
+constexpr int kDbMBs = kDbChunk / 16;
+static_assert(kDbChunk == 16 || kDbChunk == 32, "deblock chunk: one or two macroblocks");
 constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
 constexpr int kDbCW = 64, kDbCP = 66;    // chroma
 
@@ -1165,6 +1170,7 @@ __device__ __forceinline__ const uint64_t* gran_mb(FA& a, int mbx, int mby) {
 // H column and next V unit.
 struct DbState {
   int k, w0, hb0, vb0;
+  uint64_t busy = 0;  // diagnostic: time in deblock_chunk (thread 0, 10 ns ticks; only with stamps)
 };
 
 // Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
@@ -1176,13 +1182,15 @@ __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st) {
 __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st) {
   const int c1 = min((st.k + 1) * kDbChunk, a.wa);
   if (r > 0 && progress_at(&a.progress[r - 1]) < tagged(a.epoch, c1)) return false;
-  const uint64_t g = gran_ld(gran_mb(a, st.k, r) + kGranulesPerMB);  // info granule, stored last
+  // the info granule of the chunk's last macroblock (stored last; the row is coded left to right)
+  const uint64_t g = gran_ld(gran_mb(a, (c1 - 1) >> 4, r) + kGranulesPerMB);
   return (uint32_t)(g >> 32) == a.epoch;
 }
 
 // Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs).
 __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st) {
   const int tid = threadIdx.x;
+  const uint64_t tb = a.stamps && tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
   const PlaneSet cs = planes(a.recon[0]);
   const int cw = a.wa >> 1;
   const int y0 = 16 * r - 4, c0y = 8 * r - 4;  // tile origins (pixel rows)
@@ -1196,25 +1204,33 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     const int k = st.k;
     const int c0 = k * kDbChunk, c1 = min(c0 + kDbChunk, a.wa);
     const bool last = k == nch - 1;
-    // ---- inputs of chunk k: waves 0-2 the granules of MB k; wave 3 polls
-    //      row r-1's progress (rows above final through column c1), then
-    //      loads the block info and those 4 rows ----
+    // ---- inputs of chunk k: waves 0-2 the granules of its macroblocks;
+    //      wave 3 polls row r-1's progress (rows above final through column
+    //      c1), then loads the block info and those 4 rows ----
     const int hb1 = last ? a.wa : c1 - 8, vb1 = last ? a.wa : c1 - 8;
     {
-      const int m = c0 >> 4;
+      const int m0 = c0 >> 4, nmb = (c1 - c0 + 15) >> 4;  // 1 or kDbMBs macroblocks
       if (tid < kGranulesPerMB) {
-        const uint64_t* gp = gran_mb(a, m, r) + tid;
-        const uint32_t d = gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
-        int pl, row, col;
-        if (tid < 128) {
-          pl = 0, row = 4 + (tid >> 3), col = m * 16 + 2 * (tid & 7);
-        } else {
-          const int u = tid - 128;
-          pl = 1 + (u >> 5), row = 4 + ((u & 31) >> 2), col = m * 8 + 2 * (u & 3);
+        uint64_t g[kDbMBs];
+#pragma unroll
+        for (int q = 0; q < kDbMBs; q++)  // all loads issued before the first settles
+          if (q < nmb) g[q] = gran_ld(gran_mb(a, m0 + q, r) + tid);
+#pragma unroll
+        for (int q = 0; q < kDbMBs; q++) {
+          if (q >= nmb) break;
+          const int m = m0 + q;
+          const uint32_t d = gran_settle(gran_mb(a, m, r) + tid, g[q], a.epoch, a.err, a.sticky);
+          int pl, row, col;
+          if (tid < 128) {
+            pl = 0, row = 4 + (tid >> 3), col = m * 16 + 2 * (tid & 7);
+          } else {
+            const int u = tid - 128;
+            pl = 1 + (u >> 5), row = 4 + ((u & 31) >> 2), col = m * 8 + 2 * (u & 3);
+          }
+          int16_t* p = db_px(D, pl, row, col);
+          p[0] = (int16_t)(d & 0xFFFF);
+          p[1] = (int16_t)(d >> 16);
         }
-        int16_t* p = db_px(D, pl, row, col);
-        p[0] = (int16_t)(d & 0xFFFF);
-        p[1] = (int16_t)(d >> 16);
       } else {  // wave 3 (uniform loop: every lane reads the same word)
         if (r > 0 && uni((int)(progress_at(&prog[r - 1]) < (above | (uint32_t)c1)))) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1230,24 +1246,27 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
             }
           }
         }
-        if (tid < kGranulesPerMB + 2) {
-          const int row = r - 1 + (tid - kGranulesPerMB);
+        const int t3 = tid - kGranulesPerMB;  // 0..63
+        if (t3 < 2 * nmb) {  // block info of rows r-1 (0) and r (1), per macroblock
+          const int row = r - 1 + (t3 & 1), m = m0 + (t3 >> 1);
           int e = 0;
           if (row >= 0) {
             const uint64_t* gp = gran_mb(a, m, row) + kGranulesPerMB;
             e = (int)gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
           }
-          D.info[tid - kGranulesPerMB][m & 7] = (int16_t)e;
-        } else if (r > 0) {  // 4 final rows above: luma 4 x 8 dwords, chroma 2 x 4 x 4 (sc1)
-          for (int i = tid - kGranulesPerMB - 2; i < 32 + 32; i += 256 - kGranulesPerMB - 2) {
+          D.info[t3 & 1][m & 7] = (int16_t)e;
+        } else if (r > 0) {  // 4 final rows above: luma 4 x (c1-c0)/2 dwords, chroma 2 x 4 x (c1-c0)/4 (sc1)
+          const int nlw = (c1 - c0) >> 1, ncw = (c1 - c0) >> 2;
+          const int nall = 4 * nlw + 8 * ncw;
+          for (int i = t3 - 2 * nmb; i < nall; i += 64 - 2 * nmb) {
             int pl, row, col;
             const int16_t* g;
-            if (i < 32) {
-              pl = 0, row = i >> 3, col = c0 + 2 * (i & 7);
+            if (i < 4 * nlw) {
+              pl = 0, row = i / nlw, col = c0 + 2 * (i % nlw);
               g = cs.y + (size_t)(y0 + row) * a.wa + col;
             } else {
-              const int j = i - 32, pj = j >> 4, jj = j & 15;
-              pl = 1 + pj, row = jj >> 2, col = (c0 >> 1) + 2 * (jj & 3);
+              const int j = i - 4 * nlw, pj = j / (4 * ncw), jj = j % (4 * ncw);
+              pl = 1 + pj, row = jj / ncw, col = (c0 >> 1) + 2 * (jj % ncw);
               g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
             }
             const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
@@ -1264,25 +1283,27 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     //      execute in order, so no workgroup barrier between the steps ----
     if (tid < 64) {
       const int lane = tid;
-      // band A H edges of [c0, c1): luma 16 columns (lanes 0-15), chroma 2 x 8 (16-31)
-      if (r > 0 && lane < 32) {
-        if (lane < 16) {
+      constexpr int kL = kDbChunk, kC = kDbChunk / 2;  // luma / chroma columns of a whole chunk
+      // band A H edges of [c0, c1): luma kL columns, then chroma 2 x kC
+      if (r > 0 && lane < kL + 2 * kC) {
+        if (lane < kL) {
           const int col = c0 + lane;
-          db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
+          if (col < c1) db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
         } else {
-          const int pl = 1 + ((lane - 16) >> 3), col = (c0 >> 1) + (lane & 7);
-          db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
+          const int j = lane - kL, pl = 1 + j / kC, col = (c0 >> 1) + j % kC;
+          if (col < (c1 >> 1))
+            db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
         }
       }
       __builtin_amdgcn_wave_barrier();
-      // band A V edges of units c0, c0+8 (luma) and c0/2 (chroma)
-      if (lane < 16) {
+      // band A V edges of the luma units c0, c0+8, ... and the chroma units c0/2, c0/2+8, ...
+      if (lane < kL) {
         const int x = c0 + 8 * (lane >> 3), row = 4 + (lane & 7);
         if (x > 0 && x < c1)
           db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
-      } else if (lane < 32) {
-        const int pl = 1 + ((lane - 16) >> 3), x = c0 >> 1, row = 4 + (lane & 7);
-        if (x > 0)
+      } else if (lane < kL + 2 * (kC / 8) * 8) {
+        const int j = lane - kL, pl = 1 + j / kC, x = (c0 >> 1) + 8 * ((j % kC) >> 3), row = 4 + (j & 7);
+        if (x > 0 && x < (c1 >> 1))
           db_line(D, pl, false, row, x - 4, D.info[1][((x - 1) >> 3) & 7], D.info[1][(x >> 3) & 7]);
       }
       __builtin_amdgcn_wave_barrier();
@@ -1340,6 +1361,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     }
   }
   st.k++;
+  if (tb) st.busy += __builtin_amdgcn_s_memrealtime() - tb;
 }
 
 // ---------------------------------------------------------------------------
@@ -1408,7 +1430,7 @@ __device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbSt
     int d = 0;
     if (threadIdx.x == 0) {
       const bool recs = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.nref;
-      const bool can = st.k < bx && deblock_chunk_ready(a, by, st);
+      const bool can = (st.k + 1) * kDbMBs <= bx && deblock_chunk_ready(a, by, st);
       if (can && (!recs || bx - st.k > kCoderDbLag)) {
         d = 2;
       } else if (recs || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -2049,12 +2071,15 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
       __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (is) is[2] = __builtin_amdgcn_s_memrealtime();
+    int caught = 0;
     for (; !kCoderDeblock;) {  // catch the deblock up with what has arrived
       int d = 0;
       if (tid == 0) d = !kCoderDeblock && kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
       if (!wg_broadcast(vflag, d)) break;
       deblock_chunk(a, r, L.db, st);
+      caught++;
     }
+    if (is) is[11] = ((uint64_t)caught << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - is[2]);
   }
   trace(tr, 1, 1000);
   while (!kCoderDeblock && st.k < nch) {
@@ -2062,6 +2087,8 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     deblock_chunk(a, r, L.db, st);
   }
   trace(tr, 3, 100000);
+  if (a.stamps && tid == 0)  // the row's deblock time, in a per-row stamp slot no chunk uses at these widths
+    a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps + kDbStamps - 1] = st.busy;
 }
 
 // ---------------------------------------------------------------------------

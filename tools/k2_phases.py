@@ -105,6 +105,12 @@ if ok.any():
         seg = lambda a_, b_: ((ist[..., b_] - ist[..., a_])[nl2] / 100.0).mean()  # noqa: E731
         print(f"    staged -> step 16 done {seg(4, 8):.1f}, -> integer steps done {seg(8, 9):.1f}, -> sub-pel done "
               f"{seg(9, 10):.1f}, -> records released {seg(10, 2):.1f} us (first reference)")
+    if wb <= 255:  # the row's helper deblock time (last per-row stamp slot)
+        dbt = dbs[..., 255] / 100.0
+        print(f"  helper deblock per row {dbt.mean():.1f} us = {dbt.mean() / max(1, ist.shape[2]):.1f} us per group")
+    cu = ist[..., 11][ok]
+    print(f"  after each group: deblock catch-up {np.mean(cu & 0xFFFFFFFF) / 100.0:.1f} us, "
+          f"{np.mean(cu >> 32):.2f} chunks (of {(wb * 16 + 15) // 16 / max(1, ist.shape[2]):.1f} per group)")
     for j in range(B):
         okj = ist[j, ..., 2] > 0
         if okj.any() and j < 4:
