@@ -1112,8 +1112,8 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 // Column-granular deblock of MB row r (whole workgroup), trailing the row
 // coder kDbChunk luma columns (whole macroblocks) at a time: each chunk costs
 // a granule round trip, a write-through drain and a few barriers, latencies
-// that a wider chunk amortizes (16 -> 32 -> 64 columns: 4784 -> 4940 -> 5040
-// Mpix/s at 4K).  Inputs: row r's
+// that a wider chunk amortizes (16 / 32 / 64 / 80 / 96 columns:
+// 4784 / 4940 / 5040 / 4986 / 4968 Mpix/s at 4K).  Inputs: row r's
 // pre-deblock pixels and block info from its granules; the 4 pixel rows above
 // (row r-1's final output, sc1) once row r-1's progress word passes the chunk.
 // All filtering happens in a circular LDS tile (luma rows 16r-4..16r+15 x 128
@@ -1129,7 +1129,7 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 // interleaves it with the inter search), so a wide chunk delays the row's
 // progress but never stalls the helper.
 #ifndef CAIRO_DB_CHUNK
-#define CAIRO_DB_CHUNK 32
+#define CAIRO_DB_CHUNK 64
 #endif
 constexpr int kDbChunk = CAIRO_DB_CHUNK;  // luma columns per chunk: 1 to 6 macroblocks
 constexpr int kDbMBs = kDbChunk / 16;

@@ -26,6 +26,7 @@ ap.add_argument("--rows", type=int, default=0, help="row-coder workgroups (0 = d
 ap.add_argument("--helpers", type=int, default=0, help="helper workgroups of the launch (0 = default: half)")
 ap.add_argument("--row", type=int, default=10, help="MB row of the group timeline")
 ap.add_argument("--frame", type=int, default=1, help="frame (>= 1) of the batch for the lag / group-timeline sections")
+ap.add_argument("--db-chunk", type=int, default=64, help="deblock chunk width in luma columns (kernels.hip CAIRO_DB_CHUNK)")
 ap.add_argument("--dump", default="", help="also save the raw stamps (npz) here")
 a = ap.parse_args()
 w, h, ring, q = CFG[a.config]
@@ -110,7 +111,7 @@ if ok.any():
         print(f"  helper deblock per row {dbt.mean():.1f} us = {dbt.mean() / max(1, ist.shape[2]):.1f} us per group")
     cu = ist[..., 11][ok]
     print(f"  after each group: deblock catch-up {np.mean(cu & 0xFFFFFFFF) / 100.0:.1f} us, "
-          f"{np.mean(cu >> 32):.2f} chunks (of {(wb * 16 + 15) // 16 / max(1, ist.shape[2]):.1f} per group)")
+          f"{np.mean(cu >> 32):.2f} chunks (of {(wb * 16 + a.db_chunk - 1) // a.db_chunk / max(1, ist.shape[2]):.2f} per group)")
     for j in range(B):
         okj = ist[j, ..., 2] > 0
         if okj.any() and j < 4:
@@ -131,12 +132,14 @@ if B > 2:
     wt = (st[F, :, :, 1] - st[F, :, :, 0]) / 100.0
     print(f"frame {F} wait phase: at group starts mean {wt[:, 0::4].mean():.1f} us, elsewhere "
           f"{np.delete(wt, np.s_[0::4], axis=1).mean():.1f} us")
-# deblock chunk k (MB k) publish vs the coding of MB k (stamp 9)
+# deblock chunk k publish vs the coding of its last MB (stamp 9)
+CH = a.db_chunk // 16
+nch = (wb + CH - 1) // CH
 for j in range(min(B, 2)):
     for r in (3, 10, 20, hb - 1):
-        ks_ = [k for k in (2, 20, 40, 60) if k < wb]
-        print(f"  frame {j} row {r}: deblock chunk publish - MB(k) coded, us: " + "  ".join(
-            f"k={k}: {(dbs[j, r, k] - st[j, r, k, 9]) / 100.0:.1f}" for k in ks_))
+        ks_ = [k for k in (1, nch // 4, nch // 2, nch - 2) if 0 <= k < nch]
+        print(f"  frame {j} row {r}: deblock chunk k publish - its last MB coded, us: " + "  ".join(
+            f"k={k}: {(dbs[j, r, k] - st[j, r, min(CH * k + CH - 1, wb - 1), 9]) / 100.0:.1f}" for k in ks_))
 # frame 1, row 10: per group, when its inter task became ready / was claimed / done,
 # and when the row coder reached / resumed at the group's first MB
 if B > 1 and hb > 13 and (ist[..., 2] > 0).any():
@@ -144,7 +147,7 @@ if B > 1 and hb > 13 and (ist[..., 2] > 0).any():
     print(f"frame {F} row {r} per group (us): ready(deblock f{F - 1} row {r + 2}) wait-start ready done | coder reach resume")
     for g in range(0, (wb + 3) // 4, 3):
         need = min(64 * g + 80, w)  # level 1 of the inter window (kernels.hip inter_need_cols)
-        kk = [k for k in range(min(wb, 256)) if (16 * (k + 1) - 12 >= need or k == wb - 1)]
+        kk = [k for k in range(min(nch, 255)) if (a.db_chunk * (k + 1) - 12 >= need or k == nch - 1)]
         ready = (dbs[F - 1, min(r + 2, hb - 1), kk[0]] - t0) / 100.0 if kk else float("nan")
         c, rd, dn = ((ist[F, r, g, k] - t0) / 100.0 for k in range(3))
         reach, res = (st[F, r, 4 * g, 0] - t0) / 100.0, (st[F, r, 4 * g, 1] - t0) / 100.0
