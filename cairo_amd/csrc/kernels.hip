@@ -1437,7 +1437,7 @@ __device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbSt
     if (threadIdx.x == 0) {
       const bool recs = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.nref;
       const bool can = (st.k + 1) * kDbMBs <= bx && deblock_chunk_ready(a, by, st);
-      if (can && (!recs || bx - st.k > kCoderDbLag)) {
+      if (can && (!recs || bx / kDbMBs - st.k > kCoderDbLag)) {
         d = 2;
       } else if (recs || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         d = 1;

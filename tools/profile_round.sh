@@ -9,7 +9,7 @@ R=${1:-r02}; C=${2:-4k}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$C
 rm -rf $OUT && mkdir -p $OUT
-ARGS="--config $C --no-end-to-end --no-cpu-baseline --no-api"  # bench.py's default steps / warm-up
+ARGS="--config $C --no-end-to-end --no-cpu-baseline --no-api --no-host-rgb"  # bench.py's default steps / warm-up
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_kt -o run -- python3 bench.py $ARGS > $OUT/prof_kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py $ARGS > $OUT/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1
