@@ -431,6 +431,23 @@ __device__ __forceinline__ Px6 px_from_planes(const PlaneSet& p, int wa, int x, 
 __device__ __forceinline__ int lerp_px(int a, int b, int quarter) {
   return quarter ? (int16_t)(round_out(3 * a + b, 2) / 4) : (int16_t)(round_out(a + b, 1) / 2);
 }
+// The same, returned biased (v + 0x8000, so in [0, 65535]) for v_sad_u16:
+// round_out(n, h) / 2h truncates toward zero, which is (n + h - (n < 0)) >> s
+// with an arithmetic shift (h = 2^(s-1), n = a+b or 3a+b); adding 0x8000 << s
+// keeps the sum non-negative (n >= -0x8000 << s), so a logical shift yields
+// the biased value.  The reference's int16 cast never truncates here:
+// |(3a+b)/4|, |(a+b)/2| <= 0x7FFF.  4 instructions instead of 8.
+__device__ __forceinline__ uint32_t lerp_half_b(int a, int b) {
+  const int n = a + b;
+  return (uint32_t)(n + (n >> 31) + (1 + (0x8000 << 1))) >> 1;
+}
+__device__ __forceinline__ uint32_t lerp_quarter_b(int a3, int b) {  // a3 = 3a
+  const int n = a3 + b;
+  return (uint32_t)(n + (n >> 31) + (2 + (0x8000 << 2))) >> 2;
+}
+__device__ __forceinline__ uint32_t absdiff_b(uint32_t x, uint32_t y) {  // biased values
+  return __builtin_amdgcn_sad_u16(x, y, 0);
+}
 __device__ __forceinline__ Px6 lerp6(const Px6& a, const Px6& b, int q) {
   Px6 r;
   r.y0 = lerp_px(a.y0, b.y0, q);
@@ -872,6 +889,12 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
         const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
         s.sp_idx = s.sp_amt = s.sp_en = 0;
         const int bx = s.bx, by = s.by;
+        // lerps and differences in the biased domain (lerp_half_b): the
+        // source biased once, 3 * best once
+        const uint32_t sb0 = src.y0 + 0x8000, sb1 = src.y1 + 0x8000, sb2 = src.y2 + 0x8000, sb3 = src.y3 + 0x8000,
+                       sbu = src.u + 0x8000, sbv = src.v + 0x8000;
+        const int b30 = 3 * best.y0, b31 = 3 * best.y1, b32 = 3 * best.y2, b33 = 3 * best.y3, b3u = 3 * best.u,
+                  b3v = 3 * best.v;
         // accepted in the order they are evaluated (neighbour-major, half
         // then quarter), each as soon as its sums exist: no array of 16
         // results stays live (it pushed the engine into scratch spills).
@@ -889,10 +912,14 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
           const int idx = frac_index(i, j);
 #pragma unroll
           for (int q = 0; q < 2; q++) {
-            const Px6 c = lerp6(best, nb, q);
-            const int d0 = abs(src.y0 - c.y0), d1 = abs(src.y1 - c.y1), d2 = abs(src.y2 - c.y2), d3 = abs(src.y3 - c.y3);
-            const int lsum = d0 + d1 + d2 + d3;
-            const int lmax = max(max(max(d0, d1), max(d2, d3)), max(abs(src.u - c.u), abs(src.v - c.v)));
+            const uint32_t d0 = absdiff_b(sb0, q ? lerp_quarter_b(b30, nb.y0) : lerp_half_b(best.y0, nb.y0)),
+                           d1 = absdiff_b(sb1, q ? lerp_quarter_b(b31, nb.y1) : lerp_half_b(best.y1, nb.y1)),
+                           d2 = absdiff_b(sb2, q ? lerp_quarter_b(b32, nb.y2) : lerp_half_b(best.y2, nb.y2)),
+                           d3 = absdiff_b(sb3, q ? lerp_quarter_b(b33, nb.y3) : lerp_half_b(best.y3, nb.y3)),
+                           du = absdiff_b(sbu, q ? lerp_quarter_b(b3u, nb.u) : lerp_half_b(best.u, nb.u)),
+                           dv = absdiff_b(sbv, q ? lerp_quarter_b(b3v, nb.v) : lerp_half_b(best.v, nb.v));
+            const int lsum = (int)(d0 + d1 + d2 + d3);
+            const int lmax = (int)max(max(max(d0, d1), d2), max(max(d3, du), dv));
             const bool copy = s.mad < thr;
             const bool mad_lt = __ballot(lmax >= (copy ? s.mad : thr)) == 0;
             int sad = 0;
@@ -1534,7 +1561,26 @@ __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int
 }
 
 // lerp_px on both halves of two biased u16 pairs; the result as a biased pair.
+// On the biased halves a', b' directly (lerp_half_b with n = a'+b' - 0x10000
+// or 3a'+b' - 0x20000): the sign of n is bit 16 (bit 17) of the biased sum.
+#ifndef CAIRO_LERP_PAIR_B
+#define CAIRO_LERP_PAIR_B 1
+#endif
+__device__ __forceinline__ uint32_t lerp_half_bb(uint32_t a, uint32_t b) {
+  const uint32_t t = a + b;  // [0, 0x1FFFE]
+  return (t + ((t >> 16) & 1)) >> 1;
+}
+__device__ __forceinline__ uint32_t lerp_quarter_bb(uint32_t a, uint32_t b) {
+  const uint32_t t = 3 * a + b;  // [0, 0x3FFFC]
+  return (t + 1 + ((t >> 17) & 1)) >> 2;
+}
 __device__ __forceinline__ uint32_t lerp_pair(uint32_t pa, uint32_t pb, int q) {
+  if (CAIRO_LERP_PAIR_B) {
+    const uint32_t a0 = pa & 0xFFFFu, b0 = pb & 0xFFFFu, a1 = pa >> 16, b1 = pb >> 16;
+    const uint32_t l0 = q ? lerp_quarter_bb(a0, b0) : lerp_half_bb(a0, b0);
+    const uint32_t l1 = q ? lerp_quarter_bb(a1, b1) : lerp_half_bb(a1, b1);
+    return l0 | (l1 << 16);
+  }
   const uint32_t ua = pa ^ 0x80008000u, ub = pb ^ 0x80008000u;
   const int l0 = lerp_px((int16_t)ua, (int16_t)ub, q);
   const int l1 = lerp_px((int16_t)(ua >> 16), (int16_t)(ub >> 16), q);
