@@ -350,7 +350,7 @@ __device__ __forceinline__ uint4 bias4(uint4 v) {
 // origin (ox, oy) (luma pixels, multiples of 16) from plane set p, biased.
 // All 256 threads participate.
 #ifndef CAIRO_WIN_UNROLL
-#define CAIRO_WIN_UNROLL 4
+#define CAIRO_WIN_UNROLL 2
 #endif
 constexpr int kWinUnroll = CAIRO_WIN_UNROLL;
 
@@ -358,10 +358,12 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
                                             int oy, int r0, int r1, int c0, int c1) {
   // All of a thread's 16-byte loads are issued before the first LDS store
   // (kWinUnroll in flight): the staging costs one fabric round trip instead
-  // of one per chunk.
-  const int nc = (c1 - c0) >> 3, nl = (r1 - r0) * nc;  // 16-B chunks per row / in all
+  // of one per chunk.  Chunks are numbered over whole window rows (16 per
+  // luma row, 8 per chroma row) and those outside [c0, c1) skipped, so that
+  // a chunk's row and column are shifts, not divisions.
+  const int nl = (r1 - r0) << 4;
+  const int cr0 = r0 >> 1, ncl = ((r1 >> 1) - cr0) << 3;  // chroma rows [r0/2, r1/2)
   const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
-  const int ncc = nc >> 1, ncl = ((r1 >> 1) - (r0 >> 1)) * ncc;  // chroma rows [r0/2, r1/2)
   const int n = nl + 2 * ncl;
   for (int k0 = threadIdx.x; k0 < n; k0 += 256 * kWinUnroll) {
     uint4 v[kWinUnroll];
@@ -371,17 +373,17 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
       const int k = k0 + 256 * u;
       dst[u] = nullptr;
       if (k < nl) {
-        const int r = r0 + k / nc, c = c0 + (k % nc) * 8;
+        const int r = r0 + (k >> 4), c = (k & 15) << 3;
         const int gy = oy + r, gx = ox + c;
-        if (gy >= 0 && gy < ha && gx >= 0 && gx < wa) {
+        if (c >= c0 && c < c1 && gy >= 0 && gy < ha && gx >= 0 && gx < wa) {
           v[u] = *(const uint4*)&p.y[(size_t)gy * wa + gx];
           dst[u] = &w.y[r * kWinLP + c];
         }
       } else if (k < n) {
-        const int kc = k - nl, pl = kc >= ncl, kk = kc - pl * ncl;
-        const int r = (r0 >> 1) + kk / ncc, c = (c0 >> 1) + (kk % ncc) * 8;
+        const int kc = k - nl, pl = kc >= ncl, kk = kc - (pl ? ncl : 0);
+        const int r = cr0 + (kk >> 3), c = (kk & 7) << 3;
         const int gy = coy + r, gx = cox + c;
-        if (gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
+        if (2 * c >= c0 && 2 * c < c1 && gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
           v[u] = *(const uint4*)&pick(p, 1 + pl)[(size_t)gy * cw + gx];
           dst[u] = &(pl ? w.v : w.u)[r * kWinCP + c];
         }
@@ -399,17 +401,18 @@ struct Px6 {
   int y0, y1, y2, y3, u, v;
 };
 
-__device__ __forceinline__ Px6 px_from_window(const Window& w, int wx, int wy) {
+// This lane's slice of the window at (wx, wy), as raw biased values (v + 0x8000).
+__device__ __forceinline__ Px6 px_from_window_b(const Window& w, int wx, int wy) {
   int l = lane_id();
-  const int16_t* py = &w.y[(wy + (l >> 2)) * kWinLP + wx + (l & 3) * 4];
-  int cwx = wx >> 1, cwy = wy >> 1;  // caller passes window coords with the same parity as frame coords
+  const uint16_t* py = (const uint16_t*)&w.y[(wy + (l >> 2)) * kWinLP + wx + (l & 3) * 4];
+  int cwx = wx >> 1, cwy = wy >> 1;
   Px6 r;
-  r.y0 = unbias(py[0]);
-  r.y1 = unbias(py[1]);
-  r.y2 = unbias(py[2]);
-  r.y3 = unbias(py[3]);
-  r.u = unbias(w.u[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)]);
-  r.v = unbias(w.v[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)]);
+  r.y0 = py[0];
+  r.y1 = py[1];
+  r.y2 = py[2];
+  r.y3 = py[3];
+  r.u = ((const uint16_t*)w.u)[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)];
+  r.v = ((const uint16_t*)w.v)[(cwy + (l >> 3)) * kWinCP + cwx + (l & 7)];
   return r;
 }
 
@@ -431,32 +434,25 @@ __device__ __forceinline__ Px6 px_from_planes(const PlaneSet& p, int wa, int x, 
 __device__ __forceinline__ int lerp_px(int a, int b, int quarter) {
   return quarter ? (int16_t)(round_out(3 * a + b, 2) / 4) : (int16_t)(round_out(a + b, 1) / 2);
 }
-// The same, returned biased (v + 0x8000, so in [0, 65535]) for v_sad_u16:
-// round_out(n, h) / 2h truncates toward zero, which is (n + h - (n < 0)) >> s
-// with an arithmetic shift (h = 2^(s-1), n = a+b or 3a+b); adding 0x8000 << s
-// keeps the sum non-negative (n >= -0x8000 << s), so a logical shift yields
-// the biased value.  The reference's int16 cast never truncates here:
-// |(3a+b)/4|, |(a+b)/2| <= 0x7FFF.  4 instructions instead of 8.
-__device__ __forceinline__ uint32_t lerp_half_b(int a, int b) {
-  const int n = a + b;
-  return (uint32_t)(n + (n >> 31) + (1 + (0x8000 << 1))) >> 1;
+// The same on biased values (v + 0x8000, in [0, 65535]), biased result, for
+// v_sad_u16 and the packed u16 ops.  round_out(n, h) / 2h truncates toward
+// zero, which is (n + h - (n < 0)) >> s with an arithmetic shift (h =
+// 2^(s-1), n = a+b or 3a+b); on the biased sum t = a'+b' = n + 0x10000 (or
+// 3a'+b' = n + 0x20000) that is (t + h - (n < 0)) >> s, logical, and n < 0 is
+// bit 16 (bit 17) of t clear.  The reference's int16 cast never truncates
+// here: |(3a+b)/4|, |(a+b)/2| <= 0x7FFF.  4 instructions instead of 8, and no
+// unbiasing of the window values.
+__device__ __forceinline__ uint32_t lerp_half_bb(uint32_t a, uint32_t b) {
+  const uint32_t t = a + b;  // [0, 0x1FFFE]
+  return (t + ((t >> 16) & 1)) >> 1;
 }
-__device__ __forceinline__ uint32_t lerp_quarter_b(int a3, int b) {  // a3 = 3a
-  const int n = a3 + b;
-  return (uint32_t)(n + (n >> 31) + (2 + (0x8000 << 2))) >> 2;
+__device__ __forceinline__ uint32_t lerp_quarter_bb3(uint32_t a3, uint32_t b) {  // a3 = 3a'
+  const uint32_t t = a3 + b;  // [0, 0x3FFFC]
+  return (t + 1 + ((t >> 17) & 1)) >> 2;
 }
+__device__ __forceinline__ uint32_t lerp_quarter_bb(uint32_t a, uint32_t b) { return lerp_quarter_bb3(3 * a, b); }
 __device__ __forceinline__ uint32_t absdiff_b(uint32_t x, uint32_t y) {  // biased values
   return __builtin_amdgcn_sad_u16(x, y, 0);
-}
-__device__ __forceinline__ Px6 lerp6(const Px6& a, const Px6& b, int q) {
-  Px6 r;
-  r.y0 = lerp_px(a.y0, b.y0, q);
-  r.y1 = lerp_px(a.y1, b.y1, q);
-  r.y2 = lerp_px(a.y2, b.y2, q);
-  r.y3 = lerp_px(a.y3, b.y3, q);
-  r.u = lerp_px(a.u, b.u, q);
-  r.v = lerp_px(a.v, b.v, q);
-  return r;
 }
 
 // One candidate row of the inter search: a 16-lane group evaluates the
@@ -886,15 +882,15 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
         }
       } else {
         // Sub-pel: half then quarter lerp toward each of the 8 neighbours.
-        const Px6 best = px_from_window(L.win, s.bx - ox, s.by - oy);
+        // lerps and differences on the window's biased values (lerp_half_bb):
+        // the source biased once, 3 * best once
+        const Px6 best = px_from_window_b(L.win, s.bx - ox, s.by - oy);
         s.sp_idx = s.sp_amt = s.sp_en = 0;
         const int bx = s.bx, by = s.by;
-        // lerps and differences in the biased domain (lerp_half_b): the
-        // source biased once, 3 * best once
         const uint32_t sb0 = src.y0 + 0x8000, sb1 = src.y1 + 0x8000, sb2 = src.y2 + 0x8000, sb3 = src.y3 + 0x8000,
                        sbu = src.u + 0x8000, sbv = src.v + 0x8000;
-        const int b30 = 3 * best.y0, b31 = 3 * best.y1, b32 = 3 * best.y2, b33 = 3 * best.y3, b3u = 3 * best.u,
-                  b3v = 3 * best.v;
+        const uint32_t b30 = 3 * best.y0, b31 = 3 * best.y1, b32 = 3 * best.y2, b33 = 3 * best.y3, b3u = 3 * best.u,
+                       b3v = 3 * best.v;
         // accepted in the order they are evaluated (neighbour-major, half
         // then quarter), each as soon as its sums exist: no array of 16
         // results stays live (it pushed the engine into scratch spills).
@@ -908,16 +904,16 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
           const int k9 = n < 4 ? n : n + 1, i = k9 % 3 - 1, j = k9 / 3 - 1, tx = bx + i, ty = by + j;
           const bool ok = in_frame(tx, ty, a.wa, a.ha);
           if (!ok) continue;  // (wave-uniform) out of frame: not offered
-          const Px6 nb = px_from_window(L.win, tx - ox, ty - oy);
+          const Px6 nb = px_from_window_b(L.win, tx - ox, ty - oy);
           const int idx = frac_index(i, j);
 #pragma unroll
           for (int q = 0; q < 2; q++) {
-            const uint32_t d0 = absdiff_b(sb0, q ? lerp_quarter_b(b30, nb.y0) : lerp_half_b(best.y0, nb.y0)),
-                           d1 = absdiff_b(sb1, q ? lerp_quarter_b(b31, nb.y1) : lerp_half_b(best.y1, nb.y1)),
-                           d2 = absdiff_b(sb2, q ? lerp_quarter_b(b32, nb.y2) : lerp_half_b(best.y2, nb.y2)),
-                           d3 = absdiff_b(sb3, q ? lerp_quarter_b(b33, nb.y3) : lerp_half_b(best.y3, nb.y3)),
-                           du = absdiff_b(sbu, q ? lerp_quarter_b(b3u, nb.u) : lerp_half_b(best.u, nb.u)),
-                           dv = absdiff_b(sbv, q ? lerp_quarter_b(b3v, nb.v) : lerp_half_b(best.v, nb.v));
+            const uint32_t d0 = absdiff_b(sb0, q ? lerp_quarter_bb3(b30, nb.y0) : lerp_half_bb(best.y0, nb.y0)),
+                           d1 = absdiff_b(sb1, q ? lerp_quarter_bb3(b31, nb.y1) : lerp_half_bb(best.y1, nb.y1)),
+                           d2 = absdiff_b(sb2, q ? lerp_quarter_bb3(b32, nb.y2) : lerp_half_bb(best.y2, nb.y2)),
+                           d3 = absdiff_b(sb3, q ? lerp_quarter_bb3(b33, nb.y3) : lerp_half_bb(best.y3, nb.y3)),
+                           du = absdiff_b(sbu, q ? lerp_quarter_bb3(b3u, nb.u) : lerp_half_bb(best.u, nb.u)),
+                           dv = absdiff_b(sbv, q ? lerp_quarter_bb3(b3v, nb.v) : lerp_half_bb(best.v, nb.v));
             const int lsum = (int)(d0 + d1 + d2 + d3);
             const int lmax = (int)max(max(max(d0, d1), d2), max(max(d3, du), dv));
             const bool copy = s.mad < thr;
@@ -1161,6 +1157,9 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 constexpr int kDbChunk = CAIRO_DB_CHUNK;  // luma columns per chunk: 1 to 6 macroblocks
 constexpr int kDbMBs = kDbChunk / 16;
 static_assert(kDbChunk % 16 == 0 && kDbMBs >= 1 && kDbMBs <= 6, "deblock chunk: 1 to 6 macroblocks (tile width, info table)");
+// dwords per tile row in the index spaces of the rows-above loads (luma; chroma
+// half): a power of two >= kDbChunk / 2, so that row and column are shifts
+constexpr int kDbRowDw = kDbChunk <= 32 ? 16 : (kDbChunk <= 64 ? 32 : 64);
 constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
 constexpr int kDbCW = 64, kDbCP = 66;    // chroma
 
@@ -1288,16 +1287,19 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           D.info[t3 & 1][m & 7] = (int16_t)e;
         } else if (r > 0) {  // 4 final rows above: luma 4 x (c1-c0)/2 dwords, chroma 2 x 4 x (c1-c0)/4 (sc1)
           const int nlw = (c1 - c0) >> 1, ncw = (c1 - c0) >> 2;
-          const int nall = 4 * nlw + 8 * ncw;
+          constexpr int kC = kDbRowDw / 2, nall = 4 * kDbRowDw + 8 * kC;  // index space (shifts)
           for (int i = t3 - 2 * nmb; i < nall; i += 64 - 2 * nmb) {
             int pl, row, col;
             const int16_t* g;
-            if (i < 4 * nlw) {
-              pl = 0, row = i / nlw, col = c0 + 2 * (i % nlw);
+            if (i < 4 * kDbRowDw) {
+              const int d = i % kDbRowDw;
+              if (d >= nlw) continue;
+              pl = 0, row = i / kDbRowDw, col = c0 + 2 * d;
               g = cs.y + (size_t)(y0 + row) * a.wa + col;
             } else {
-              const int j = i - 4 * nlw, pj = j / (4 * ncw), jj = j % (4 * ncw);
-              pl = 1 + pj, row = jj / ncw, col = (c0 >> 1) + 2 * (jj % ncw);
+              const int j = i - 4 * kDbRowDw, pj = j / (4 * kC), jj = j % (4 * kC), d = jj % kC;
+              if (d >= ncw) continue;
+              pl = 1 + pj, row = jj / kC, col = (c0 >> 1) + 2 * d;
               g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
             }
             const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
@@ -1358,15 +1360,22 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
       const int rl0 = r > 0 ? 1 : 4, rc0 = r > 0 ? 1 : 4;  // first tile row written
       const int nl = (w1 - w0) >> 1, nc = (w1 - w0) >> 2;
       const int nrl = 20 - rl0, nrc = 12 - rc0;
-      for (int i = tid; i < nrl * nl + 2 * nrc * nc; i += 256) {
+      // index space: per row, sl = 1 or 2 bands of 32 dwords (luma; chroma 16),
+      // so that row, band and column are shifts and masks
+      const int sl = nl > 32 ? 1 : 0, sc = nc > 16 ? 1 : 0;
+      const int NL = nrl << (5 + sl), NC = nrc << (4 + sc);
+      for (int i = tid; i < NL + 2 * NC; i += 256) {
         int pl, row, col;
         int16_t* g;
-        if (i < nrl * nl) {
-          pl = 0, row = rl0 + i / nl, col = w0 + 2 * (i % nl);
+        if (i < NL) {
+          const int d = i & ((32 << sl) - 1);
+          if (d >= nl) continue;
+          pl = 0, row = rl0 + (i >> (5 + sl)), col = w0 + 2 * d;
           g = cs.y + (size_t)(y0 + row) * a.wa + col;
         } else {
-          const int j = i - nrl * nl, pj = j / (nrc * nc), jj = j % (nrc * nc);
-          pl = 1 + pj, row = rc0 + jj / nc, col = (w0 >> 1) + 2 * (jj % nc);
+          const int j = i - NL, pj = j >= NC, jj = j - (pj ? NC : 0), d = jj & ((16 << sc) - 1);
+          if (d >= nc) continue;
+          pl = 1 + pj, row = rc0 + (jj >> (4 + sc)), col = (w0 >> 1) + 2 * d;
           g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
         }
         const int16_t* p = db_px(D, pl, row, col);
@@ -1561,19 +1570,10 @@ __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int
 }
 
 // lerp_px on both halves of two biased u16 pairs; the result as a biased pair.
-// On the biased halves a', b' directly (lerp_half_b with n = a'+b' - 0x10000
-// or 3a'+b' - 0x20000): the sign of n is bit 16 (bit 17) of the biased sum.
+// On the biased halves directly (lerp_half_bb).
 #ifndef CAIRO_LERP_PAIR_B
 #define CAIRO_LERP_PAIR_B 1
 #endif
-__device__ __forceinline__ uint32_t lerp_half_bb(uint32_t a, uint32_t b) {
-  const uint32_t t = a + b;  // [0, 0x1FFFE]
-  return (t + ((t >> 16) & 1)) >> 1;
-}
-__device__ __forceinline__ uint32_t lerp_quarter_bb(uint32_t a, uint32_t b) {
-  const uint32_t t = 3 * a + b;  // [0, 0x3FFFC]
-  return (t + 1 + ((t >> 17) & 1)) >> 2;
-}
 __device__ __forceinline__ uint32_t lerp_pair(uint32_t pa, uint32_t pb, int q) {
   if (CAIRO_LERP_PAIR_B) {
     const uint32_t a0 = pa & 0xFFFFu, b0 = pb & 0xFFFFu, a1 = pa >> 16, b1 = pb >> 16;
