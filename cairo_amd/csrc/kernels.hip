@@ -705,7 +705,7 @@ __device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
 struct DbLds;
 struct DbState;
 __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st);
-__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st);
+__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st, bool known_ready = false);
 __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st);
 
 // Helper wait (whole workgroup): until the deblock progress of frame
@@ -713,6 +713,7 @@ __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st);
 // reaches need, running this row's ready deblock chunks meanwhile; then
 // acquire what the progress word released.  Bounded like every wait (the
 // error word ends it).
+template <bool kDeblock = true>
 __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int need, DbLds& D,
                                             DbState& st, int* flag) {
   volatile int* vflag = flag;
@@ -723,7 +724,8 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
     if (threadIdx.x == 0) {
       if (!pp || progress_peer(a.sys, pp + rr) >= tagged(a.epoch - back, need)) {
         d = 1;
-      } else if (!kCoderDeblock && kHelperInterleave && deblock_pending(a, st) && deblock_chunk_ready(a, r, st)) {
+      } else if (kDeblock && !kCoderDeblock && kHelperInterleave && deblock_pending(a, st) &&
+                 deblock_chunk_ready(a, r, st)) {
         d = 2;
       } else {  // nothing to do: back off
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -740,7 +742,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
     }
     d = wg_broadcast(vflag, d);
     if (d == 1) break;
-    if (d == 2) deblock_chunk(a, r, D, st);
+    if (kDeblock && d == 2) deblock_chunk(a, r, D, st, true);
   }
   if (threadIdx.x == 0) {  // the check used a relaxed load: acquire what it observed
     acquire_fence(a.sys);
@@ -835,8 +837,10 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
         lvl2_open = (m4 >> 2) != 0;
         if (m) {
           if (is) is[5] = __builtin_amdgcn_s_memrealtime();
-          helper_wait(a, off == 1 ? 1 : 2, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2), D, st,
-                      flag);
+          // (no deblock meanwhile: rare, and its inputs' registers would spill
+          // the search state live here)
+          helper_wait<false>(a, off == 1 ? 1 : 2, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2),
+                             D, st, flag);
           if (m & 2) load_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
           if (!lvl2c) load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
           __syncthreads();
@@ -1196,11 +1200,20 @@ __device__ __forceinline__ const uint64_t* gran_mb(FA& a, int mbx, int mby) {
   return a.granules + (size_t)(mby * a.wmb + mbx) * kGranuleStride;
 }
 
+// Per-phase deblock times in the stamps (tools/k2_phases.py); off by default:
+// the extra live values cost VGPR spills.
+#ifndef CAIRO_DB_PHASES
+#define CAIRO_DB_PHASES 0
+#endif
+
 // Deblock progress of one MB row: next chunk, columns written, band B's next
 // H column and next V unit.
 struct DbState {
   int k, w0, hb0, vb0;
   uint64_t busy = 0;  // diagnostic: time in deblock_chunk (thread 0, 10 ns ticks; only with stamps)
+#if CAIRO_DB_PHASES
+  uint64_t ph[3] = {0, 0, 0};  // diagnostic: of which inputs, filters, write-out issue (the rest: drain)
+#endif
 };
 
 // Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
@@ -1217,8 +1230,9 @@ __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState&
   return (uint32_t)(g >> 32) == a.epoch;
 }
 
-// Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs).
-__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st) {
+// Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs, or
+// known_ready: deblock_chunk_ready said so).
+__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st, bool known_ready) {
   const int tid = threadIdx.x;
   const uint64_t tb = a.stamps && tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
   const PlaneSet cs = planes(a.recon[0]);
@@ -1262,7 +1276,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           p[1] = (int16_t)(d >> 16);
         }
       } else {  // wave 3 (uniform loop: every lane reads the same word)
-        if (r > 0 && uni((int)(progress_at(&prog[r - 1]) < (above | (uint32_t)c1)))) {
+        if (r > 0 && !known_ready && uni((int)(progress_at(&prog[r - 1]) < (above | (uint32_t)c1)))) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           while (uni((int)(progress_at(&prog[r - 1]) < (above | (uint32_t)c1)))) {
             if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
@@ -1312,6 +1326,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
       }
     }
     __syncthreads();
+    const uint64_t t1 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---- the filters, in order, by wave 0 alone: a wave's LDS accesses
     //      execute in order, so no workgroup barrier between the steps ----
     if (tid < 64) {
@@ -1352,6 +1367,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
       }
     }
     __syncthreads();
+    const uint64_t t2 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
     hb0 = max(hb0, hb1);
     vb0 = max(vb0, vb1);
     const int w1 = last ? a.wa : max(w0, c1 - 12);
@@ -1387,8 +1403,14 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(pick(planes(a.push[q]), pl) + off), d,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
+      const uint64_t t3 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+#if CAIRO_DB_PHASES
+      if (tb) st.ph[0] += t1 - tb, st.ph[1] += t2 - t1, st.ph[2] += t3 - t2;
+#else
+      (void)t1, (void)t2, (void)t3;
+#endif
       if (tid == 0) {
         if (a.sys) {  // the next frame may read this row from another device
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -1490,7 +1512,7 @@ __device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbSt
     }
     d = wg_broadcast(vflag, d);
     if (d == 1) break;
-    if (d == 2) deblock_chunk(a, by, D, st);
+    if (d == 2) deblock_chunk(a, by, D, st, true);
   }
 }
 
@@ -2128,7 +2150,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
       int d = 0;
       if (tid == 0) d = !kCoderDeblock && kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
       if (!wg_broadcast(vflag, d)) break;
-      deblock_chunk(a, r, L.db, st);
+      deblock_chunk(a, r, L.db, st, true);
       caught++;
     }
     if (is) is[11] = ((uint64_t)caught << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - is[2]);
@@ -2139,8 +2161,13 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     deblock_chunk(a, r, L.db, st);
   }
   trace(tr, 3, 100000);
-  if (a.stamps && tid == 0)  // the row's deblock time, in a per-row stamp slot no chunk uses at these widths
-    a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps + kDbStamps - 1] = st.busy;
+  if (a.stamps && tid == 0) {  // the row's deblock times, in per-row stamp slots no chunk uses at these widths
+    uint64_t* ds = a.stamps + (size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps;
+    ds[kDbStamps - 1] = st.busy;
+#if CAIRO_DB_PHASES
+    ds[kDbStamps - 2] = st.ph[0], ds[kDbStamps - 3] = st.ph[1], ds[kDbStamps - 4] = st.ph[2];
+#endif
+  }
 }
 
 // ---------------------------------------------------------------------------
