@@ -139,6 +139,7 @@ struct FrameArgs {
   // scope, with a system-scope release before each store and a system-scope
   // acquire after each wait on another frame's data.
   int sys;
+  int db_shift;        // deblock chunk width, log2 luma columns (4..6: 1, 2 or 4 macroblocks)
   uint64_t* stamps;    // diagnostic (nullptr = off)
   uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, kIStamps stamps (see kernels.hip)
   const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)

@@ -1137,7 +1137,8 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 }
 
 // Column-granular deblock of MB row r (whole workgroup), trailing the row
-// coder kDbChunk luma columns (whole macroblocks) at a time: each chunk costs
+// coder one chunk of 2^db_shift luma columns (whole macroblocks) at a time
+// (FrameArgs::db_shift, make_frame_view): each chunk costs
 // a granule round trip, a write-through drain and a few barriers, latencies
 // that a wider chunk amortizes (16 / 32 / 64 / 80 / 96 columns:
 // 4784 / 4940 / 5040 / 4986 / 4968 Mpix/s at 4K).  Inputs: row r's
@@ -1155,15 +1156,14 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 // chunk ahead; a chunk runs only once its inputs are present (the helper
 // interleaves it with the inter search), so a wide chunk delays the row's
 // progress but never stalls the helper.
+// The chunk width is per frame (FrameArgs::db_shift, make_frame_view): 0
+// picks it by frame width, CAIRO_DB_CHUNK = 16 / 32 / 64 forces one.
 #ifndef CAIRO_DB_CHUNK
-#define CAIRO_DB_CHUNK 64
+#define CAIRO_DB_CHUNK 0
 #endif
-constexpr int kDbChunk = CAIRO_DB_CHUNK;  // luma columns per chunk: 1 to 6 macroblocks
+constexpr int kDbChunk = 64;  // the widest chunk: luma columns (tile width, info table, arrays)
 constexpr int kDbMBs = kDbChunk / 16;
-static_assert(kDbChunk % 16 == 0 && kDbMBs >= 1 && kDbMBs <= 6, "deblock chunk: 1 to 6 macroblocks (tile width, info table)");
-// dwords per tile row in the index spaces of the rows-above loads (luma; chroma
-// half): a power of two >= kDbChunk / 2, so that row and column are shifts
-constexpr int kDbRowDw = kDbChunk <= 32 ? 16 : (kDbChunk <= 64 ? 32 : 64);
+__device__ __forceinline__ int db_chunks(const FA& a) { return (a.wa + (1 << a.db_shift) - 1) >> a.db_shift; }
 constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
 constexpr int kDbCW = 64, kDbCP = 66;    // chroma
 
@@ -1219,11 +1219,11 @@ struct DbState {
 // Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
 // Evaluated by thread 0 only.
 __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st) {
-  return st.k < (a.wa + kDbChunk - 1) / kDbChunk;
+  return st.k < db_chunks(a);
 }
 
 __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st) {
-  const int c1 = min((st.k + 1) * kDbChunk, a.wa);
+  const int c1 = min((st.k + 1) << a.db_shift, a.wa);
   if (r > 0 && progress_at(&a.progress[r - 1]) < tagged(a.epoch, c1)) return false;
   // the info granule of the chunk's last macroblock (stored last; the row is coded left to right)
   const uint64_t g = gran_ld(gran_mb(a, (c1 - 1) >> 4, r) + kGranulesPerMB);
@@ -1238,7 +1238,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
   const PlaneSet cs = planes(a.recon[0]);
   const int cw = a.wa >> 1;
   const int y0 = 16 * r - 4, c0y = 8 * r - 4;  // tile origins (pixel rows)
-  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  const int nch = db_chunks(a);
   uint64_t* prog = a.progress;
   const uint64_t above = tagged(a.epoch, 0);
   int& w0 = st.w0;
@@ -1246,14 +1246,14 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
   int& vb0 = st.vb0;
   {
     const int k = st.k;
-    const int c0 = k * kDbChunk, c1 = min(c0 + kDbChunk, a.wa);
+    const int c0 = k << a.db_shift, c1 = min(c0 + (1 << a.db_shift), a.wa);
     const bool last = k == nch - 1;
     // ---- inputs of chunk k: waves 0-2 the granules of its macroblocks;
     //      wave 3 polls row r-1's progress (rows above final through column
     //      c1), then loads the block info and those 4 rows ----
     const int hb1 = last ? a.wa : c1 - 8, vb1 = last ? a.wa : c1 - 8;
     {
-      const int m0 = c0 >> 4, nmb = (c1 - c0 + 15) >> 4;  // 1 or kDbMBs macroblocks
+      const int m0 = c0 >> 4, nmb = (c1 - c0 + 15) >> 4;  // 1 to kDbMBs macroblocks
       if (tid < kGranulesPerMB) {
         uint64_t g[kDbMBs];
 #pragma unroll
@@ -1301,19 +1301,21 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           D.info[t3 & 1][m & 7] = (int16_t)e;
         } else if (r > 0) {  // 4 final rows above: luma 4 x (c1-c0)/2 dwords, chroma 2 x 4 x (c1-c0)/4 (sc1)
           const int nlw = (c1 - c0) >> 1, ncw = (c1 - c0) >> 2;
-          constexpr int kC = kDbRowDw / 2, nall = 4 * kDbRowDw + 8 * kC;  // index space (shifts)
+          // index space: a whole chunk's dwords per row (luma 2^(s-1), chroma
+          // 2^(s-2)), so that row and column are shifts
+          const int s1 = a.db_shift - 1, s2 = a.db_shift - 2, nall = 8 << s1;
           for (int i = t3 - 2 * nmb; i < nall; i += 64 - 2 * nmb) {
             int pl, row, col;
             const int16_t* g;
-            if (i < 4 * kDbRowDw) {
-              const int d = i % kDbRowDw;
+            if (i < (4 << s1)) {
+              const int d = i & ((1 << s1) - 1);
               if (d >= nlw) continue;
-              pl = 0, row = i / kDbRowDw, col = c0 + 2 * d;
+              pl = 0, row = i >> s1, col = c0 + 2 * d;
               g = cs.y + (size_t)(y0 + row) * a.wa + col;
             } else {
-              const int j = i - 4 * kDbRowDw, pj = j / (4 * kC), jj = j % (4 * kC), d = jj % kC;
+              const int j = i - (4 << s1), pj = j >> (s2 + 2), jj = j & ((4 << s2) - 1), d = jj & ((1 << s2) - 1);
               if (d >= ncw) continue;
-              pl = 1 + pj, row = jj / kC, col = (c0 >> 1) + 2 * d;
+              pl = 1 + pj, row = jj >> s2, col = (c0 >> 1) + 2 * d;
               g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
             }
             const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
@@ -1331,14 +1333,14 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     //      execute in order, so no workgroup barrier between the steps ----
     if (tid < 64) {
       const int lane = tid;
-      constexpr int kL = kDbChunk, kC = kDbChunk / 2;  // luma / chroma columns of a whole chunk
+      const int ls = a.db_shift, kL = 1 << ls, kC = kL >> 1;  // luma / chroma columns of a whole chunk
       // band A H edges of [c0, c1): luma kL columns, then chroma 2 x kC
       for (int i = lane; r > 0 && i < kL + 2 * kC; i += 64) {
         if (i < kL) {
           const int col = c0 + i;
           if (col < c1) db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
         } else {
-          const int j = i - kL, pl = 1 + j / kC, col = (c0 >> 1) + j % kC;
+          const int j = i - kL, pl = 1 + (j >> (ls - 1)), col = (c0 >> 1) + (j & (kC - 1));
           if (col < (c1 >> 1))
             db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
         }
@@ -1351,7 +1353,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           if (x > 0 && x < c1)
             db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
         } else {
-          const int j = i - kL, pl = 1 + j / kC, x = (c0 >> 1) + 8 * ((j % kC) >> 3), row = 4 + (j & 7);
+          const int j = i - kL, pl = 1 + (j >> (ls - 1)), x = (c0 >> 1) + 8 * ((j & (kC - 1)) >> 3), row = 4 + (j & 7);
           if (x > 0 && x < (c1 >> 1))
             db_line(D, pl, false, row, x - 4, D.info[1][((x - 1) >> 3) & 7], D.info[1][(x >> 3) & 7]);
         }
@@ -1494,8 +1496,8 @@ __device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbSt
     int d = 0;
     if (threadIdx.x == 0) {
       const bool recs = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.nref;
-      const bool can = (st.k + 1) * kDbMBs <= bx && deblock_chunk_ready(a, by, st);
-      if (can && (!recs || bx / kDbMBs - st.k > kCoderDbLag)) {
+      const bool can = ((st.k + 1) << (a.db_shift - 4)) <= bx && deblock_chunk_ready(a, by, st);
+      if (can && (!recs || (bx >> (a.db_shift - 4)) - st.k > kCoderDbLag)) {
         d = 2;
       } else if (recs || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         d = 1;
@@ -2088,7 +2090,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
   }
 #if CAIRO_CODER_DEBLOCK
   // the rest of the row's deblock (each chunk waits for the row above)
-  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  const int nch = db_chunks(a);
   while (dst.k < nch) deblock_chunk(a, by, L.db, dst);
 #endif
 }
@@ -2116,7 +2118,7 @@ struct EngineLds {
 // or done).  Never blocks on its own row coder while an inter group is due.
 __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag, int32_t* tr) {
   const int tid = threadIdx.x;
-  const int nch = (a.wa + kDbChunk - 1) / kDbChunk;
+  const int nch = db_chunks(a);
   volatile int* vflag = flag;
   DbState st{0, 0, 0, 8};
   for (int g = 0; g < a.ng; g++) {
@@ -2348,6 +2350,13 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.npush = f.npush;
   for (int k = 0; k < kMaxPush; k++) a.push[k] = f.push[k];
   a.sys = f.sys;
+  // deblock chunk width: a wider chunk amortizes the chunk's fixed latencies
+  // (granule round trip, drain, barriers) over more columns but publishes the
+  // row's progress later, which the next frame's searches wait for; narrow
+  // frames feel the latter more (A/B, Mpix/s, chunk 16 / 32 / 64: 720p
+  // 3859-3870 / 3384-3435 / 2893-2916, 1080p 4549 / 4660 / 4133, 4K 4784 /
+  // 4940 / 5040)
+  a.db_shift = CAIRO_DB_CHUNK ? __builtin_ctz(CAIRO_DB_CHUNK) : (e.wmb >= 200 ? 6 : e.wmb >= 100 ? 5 : 4);
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   {
     const int ng = (e.wmb + 3) / 4;
