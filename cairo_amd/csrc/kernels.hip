@@ -329,7 +329,15 @@ __device__ __forceinline__ void pk_diff(uint32_t a, uint32_t b, uint32_t& sad, u
 // every candidate the searches can reach.
 // ---------------------------------------------------------------------------
 
-constexpr int kWinL = 80, kWinLW = 128, kWinLP = 136;  // luma rows, width, pitch (elements)
+// Luma pitch: 136 elements = 68 dwords puts rows i and i+8 of a candidate's
+// 16-lane group on one bank (ds_read_b32 banks are dword mod 32); 140 = 70
+// dwords spreads 16 rows over 16 banks, at the price of 8-byte (not 16-byte)
+// aligned rows for the staging stores.
+#ifndef CAIRO_WIN_PITCH
+#define CAIRO_WIN_PITCH 136
+#endif
+constexpr int kWinL = 80, kWinLW = 128, kWinLP = CAIRO_WIN_PITCH;  // luma rows, width, pitch (elements)
+static_assert(kWinLP % 4 == 0 || kWinLP % 4 == 2, "window rows 4- or 8-byte aligned");
 constexpr int kWinC = 40, kWinCP = 72;  // chroma rows, pitch (64 columns)
 
 struct alignas(16) Window {
@@ -391,7 +399,15 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
     }
 #pragma unroll
     for (int u = 0; u < kWinUnroll; u++)
-      if (dst[u]) *(uint4*)dst[u] = bias4(v[u]);
+      if (dst[u]) {
+        const uint4 b = bias4(v[u]);
+        if (kWinLP % 8 == 0) {
+          *(uint4*)dst[u] = b;
+        } else {  // 8-byte aligned rows (chroma rows stay 16-byte aligned; the same stores serve both)
+          ((uint2*)dst[u])[0] = make_uint2(b.x, b.y);
+          ((uint2*)dst[u])[1] = make_uint2(b.z, b.w);
+        }
+      }
   }
 }
 
@@ -751,12 +767,88 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
   __syncthreads();
 }
 
+#ifndef CAIRO_DB_IN_WAIT1
+#define CAIRO_DB_IN_WAIT1 1
+#endif
+#ifndef CAIRO_GROUP_SOURCE
+#define CAIRO_GROUP_SOURCE 1
+#endif
+constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
+
 struct InterLds {
   Window win;
   int need[4];
   int full;  // the whole window is final (staged at once)
   int lvl2[6][4];  // per step (16, 8, 4, 2, 1, sub-pel) and wave: level 2 wanted
+  // the group's source macroblocks (raw int16: 16x16 luma, 8x8 U, 8x8 V per
+  // wave), loaded once per group; the zero-MV SAD / MAD of the older
+  // references, computed together at the group start
+  alignas(16) int16_t src[4][384];
+  int zsad[kMaxRing][4], zmad[kMaxRing][4];
 };
+
+// Wave w's source macroblock (4g + w, r) into L.src[w], row-major: luma
+// 16 x 16, then U 8 x 8, then V 8 x 8; lanes 0..47 one 16-byte chunk each (a
+// luma half row, a chroma row).  Only this wave reads it back (its LDS
+// operations execute in order: no barrier).
+__device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, x = 4 * g + wave;
+  if (x >= a.wmb || lane >= 48) return;
+  const PlaneSet in = planes(a.in);
+  const int px = x * kMB, py = r * kMB;
+  const int16_t* gsrc;
+  if (lane < 32) {  // luma row lane >> 1, half lane & 1
+    gsrc = in.y + (size_t)(py + (lane >> 1)) * a.wa + px + 8 * (lane & 1);
+  } else {  // chroma: 16 chunks, U rows 0..7 then V rows 0..7
+    const int k = lane - 32;
+    gsrc = pick(in, 1 + (k >> 3)) + (size_t)((py >> 1) + (k & 7)) * (a.wa >> 1) + (px >> 1);
+  }
+  *(uint4*)&L.src[wave][8 * lane] = *(const uint4*)gsrc;
+}
+
+// This lane's Px6 slice (px_from_planes layout) and its SrcRow (load_src_rows
+// layout, biased) of wave w's source macroblock, from L.src.
+__device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int wave) {
+  const int l = threadIdx.x & 63;
+  const int16_t* m = L.src[wave];
+  Px6 p;
+  const int16_t* y = &m[(l >> 2) * 16 + (l & 3) * 4];
+  p.y0 = y[0], p.y1 = y[1], p.y2 = y[2], p.y3 = y[3];
+  p.u = m[256 + (l >> 3) * 8 + (l & 7)];
+  p.v = m[320 + (l >> 3) * 8 + (l & 7)];
+  return p;
+}
+__device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int wave, int i) {
+  const uint32_t* m = (const uint32_t*)L.src[wave];
+  SrcRow s;
+#pragma unroll
+  for (int k = 0; k < 8; k++) s.y[k] = m[i * 8 + k] ^ 0x80008000u;
+  const int co = (i >> 1) * 4 + (i & 1) * 2;  // dwords: row i>>1 of 8 px = 4 dwords, half i&1
+  s.u[0] = m[128 + co] ^ 0x80008000u, s.u[1] = m[128 + co + 1] ^ 0x80008000u;
+  s.v[0] = m[160 + co] ^ 0x80008000u, s.v[1] = m[160 + co + 1] ^ 0x80008000u;
+  return s;
+}
+
+// The zero-MV SAD / MAD of references 2..nref for the group (all loads of a
+// wave issued together), into L.zsad / L.zmad.  After the wait for frame
+// index-2's level-1 window (which covers the zero-MV block).
+__device__ __forceinline__ void zero_mv_older(FA& a, int r, int g, InterLds& L) {
+  const int wave = threadIdx.x >> 6, x = 4 * g + wave;
+  if (x >= a.wmb) return;
+  const int px = x * kMB, py = r * kMB;
+  const Px6 src = src_px_lds(L, wave);
+  Px6 ref[kMaxRing - 1];
+#pragma unroll
+  for (int off = 2; off < kMaxRing; off++)
+    if (off <= a.nref) ref[off - 1] = px_from_planes(RECON_AT(a, off), a.wa, px, py);
+#pragma unroll
+  for (int off = 2; off < kMaxRing; off++) {
+    if (off > a.nref) break;
+    int sad, mad;
+    sad_mad(src, ref[off - 1], sad, mad);
+    if ((threadIdx.x & 63) == 0) L.zsad[off][wave] = sad, L.zmad[off][wave] = mad;
+  }
+}
 
 // Need of the group's level-1 / level-2 windows: (MB row whose deblock
 // progress counts, luma columns).
@@ -784,7 +876,15 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   s.sp_idx = s.sp_amt = s.sp_en = 0;
   s.sad = s.mad = 0;
   SrcRow srow;  // biased source rows of this lane's group slot (integer steps)
-  if (valid) {  // zero-MV candidate straight from the planes
+  if (valid && kGroupSource) {  // the source from the group's LDS copy
+    src = src_px_lds(L, wave);
+    srow = src_rows_lds(L, wave, threadIdx.x & 15);
+    if (off >= 2) {  // zero-MV computed at the group start
+      s.sad = L.zsad[off][wave], s.mad = L.zmad[off][wave];
+    } else {  // zero-MV candidate straight from the planes
+      sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
+    }
+  } else if (valid) {  // zero-MV candidate straight from the planes
     src = px_from_planes(planes(a.in), a.wa, px, py);
     sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
     srow = load_src_rows(planes(a.in), a.wa, px, py, threadIdx.x & 15);
@@ -2131,12 +2231,17 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     // progress word, tagged epoch-2, also covers frame index-3: that frame's
     // row r+2 waited for index-3's row r+4 over a wider window), so these
     // searches fill what used to be the wait for the previous frame.
+    if (kGroupSource && a.inter) group_source(a, r, g, L.inter);
     if (a.inter && a.nref >= 2) {
       helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+      if (kGroupSource) zero_mv_older(a, r, g, L.inter);
       for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is, 0);
     }
     // level 1 of the group's window in the previous frame; deblock meanwhile
-    helper_wait(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+    // (a deblock chunk started here delays the search when the previous
+    // frame's progress arrives meanwhile: CAIRO_DB_IN_WAIT1 = 0 leaves the
+    // chunks to the catch-up after the group's records)
+    helper_wait<CAIRO_DB_IN_WAIT1 != 0>(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
