@@ -75,6 +75,21 @@ __constant__ int16_t kBeta[32] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 3
 // with a per-lane index is then an LDS read (lgkmcnt) instead of a global load
 // whose vmcnt(0) wait would also drain the outstanding hand-off loads.
 __shared__ int16_t sLut8[64], sQmIntra[64], sQmInter[64], sAlpha[32], sBeta[32];
+// Reciprocals for the quantizer's divisions (rdiv_m): the matrices' entries,
+// 2 qp and the DC scales for qp = 0..31.
+__shared__ uint32_t sMagQmIntra[64], sMagQmInter[64], sMag2qp[32], sMagDcL[32], sMagDcC[32];
+
+// m = ceil(2^32 / d) for 2 <= d: then u / d = mulhi(u, m) exactly for u * d <
+// 2^32 (the error term u * (m d - 2^32) / 2^32 stays below 1 / d).
+__host__ __device__ inline uint32_t div_magic(uint32_t d) { return 0xFFFFFFFFu / d + 1u; }
+// rdiv (rounded_div, half away from zero) by d > 1 with its div_magic m, for
+// |n| + d / 2 < 2^32 / d: sign(n) * ((|n| + d/2) / d), which is rdiv's
+// truncating division of n -/+ d/2.  One mulhi instead of a division.
+__device__ __forceinline__ int32_t rdiv_m(int32_t n, int32_t d, uint32_t m) {
+  const uint32_t u = (uint32_t)(n < 0 ? -n : n) + (uint32_t)(d >> 1);
+  const int32_t q = (int32_t)__umulhi(u, m);
+  return n < 0 ? -q : q;
+}
 
 // Whole workgroup; ends with a barrier.
 __device__ __forceinline__ void load_tables() {
@@ -86,6 +101,14 @@ __device__ __forceinline__ void load_tables() {
   } else if (t < 96) {
     sAlpha[t - 64] = kAlpha[t - 64];
     sBeta[t - 64] = kBeta[t - 64];
+  } else if (t < 128) {
+    const int q = t - 96;
+    sMag2qp[q] = div_magic(max(2 * q, 2));
+    sMagDcL[q] = div_magic(luma_dc_scale(q));
+    sMagDcC[q] = div_magic(chroma_dc_scale(q));
+  } else if (t < 192) {
+    sMagQmIntra[t - 128] = div_magic(kQmIntra[t - 128]);
+    sMagQmInter[t - 128] = div_magic(kQmInter[t - 128]);
   }
   __syncthreads();
 }
@@ -1169,14 +1192,17 @@ __device__ __forceinline__ int vaq_mb(int32_t* red, int wave, int lane, int coef
 }
 
 // quantize_macroblock (quantize.cpp:357-367): element-wise.
+// The divisions by reciprocal (rdiv_m; qp is 1..31, |c| < 2^15, the
+// divisors at most 62: every quotient exact).
 __device__ __forceinline__ int16_t quant_elem(int e, int32_t c, int qp, bool intra_path) {
   int b = e >> 6, k = e & 63;
   if (intra_path) {
-    if (k == 0) return (int16_t)rdiv(c, b < 4 ? luma_dc_scale(qp) : chroma_dc_scale(qp));
-    return (int16_t)rdiv(rdiv(c * kQScale, sQmIntra[k]), qp << 1);
+    if (k == 0)
+      return (int16_t)(b < 4 ? rdiv_m(c, luma_dc_scale(qp), sMagDcL[qp]) : rdiv_m(c, chroma_dc_scale(qp), sMagDcC[qp]));
+    return (int16_t)rdiv_m(rdiv_m(c * kQScale, sQmIntra[k], sMagQmIntra[k]), qp << 1, sMag2qp[qp]);
   }
-  int16_t qf = (int16_t)rdiv(c * kQScale, sQmInter[k]);
-  return (int16_t)rdiv(qf - sign16(qf) * qp, qp << 1);
+  int16_t qf = (int16_t)rdiv_m(c * kQScale, sQmInter[k], sMagQmInter[k]);
+  return (int16_t)rdiv_m(qf - sign16(qf) * qp, qp << 1, sMag2qp[qp]);
 }
 // inverse_quantize_macroblock (quantize.cpp:369-379): element-wise.
 __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool intra_path) {
