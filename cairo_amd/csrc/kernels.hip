@@ -2028,15 +2028,17 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         stamp(a, mb, 3);
         {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
           const int bx0 = sel.bx, by0 = sel.by;
-          const int nn = grp >> 1, q = grp & 1;
+          // candidate c = 2 nn + q; q is wave-uniform (waves 0 and 2 the half
+          // steps, 1 and 3 the quarter steps), so a wave runs one lerp, not both
+          const int q = (grp >> 2) & 1, nn = (grp & 3) | ((grp >> 3) << 2), c = 2 * nn + q;
           const int k9 = nn < 4 ? nn : nn + 1;  // skip the centre of the 3x3
           const int tx = bx0 + k9 % 3 - 1, ty = by0 + k9 / 3 - 1;
           const bool ok = intra_valid(tx, ty, px, py, a.wa, a.ha);
           int sad, mad;
-          subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, q, gi, s, sad, mad);
+          subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, uni(q), gi, s, sad, mad);
           if (gi == 0) {
-            L.cand[buf][grp][0] = ok ? sad : -1;
-            L.cand[buf][grp][1] = mad;
+            L.cand[buf][c][0] = ok ? sad : -1;
+            L.cand[buf][c][1] = mad;
           }
           __syncthreads();
           const int vs = L.cand[buf][lane & 15][0], vm = L.cand[buf][lane & 15][1];
