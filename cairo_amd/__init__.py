@@ -97,6 +97,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_max_workgroups": (I, [P]),
         "cairo_default_batch": (I, [U, U]),
         "cairo_task_order": (I, [I, I, P, ctypes.POINTER(I)]),
+        "cairo_task_queues": (I, [I, I, P, P, ctypes.POINTER(I)]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "cairo_serialize_feed": (I, [P, ctypes.c_uint64, P, U, ctypes.POINTER(U)]),
@@ -495,6 +496,16 @@ def task_order(hmb: int, frames: int):
     slope = ctypes.c_int()
     _ck(lib().cairo_task_order(hmb, frames, _ptr(out), ctypes.byref(slope)), "cairo_task_order")
     return out, slope.value
+
+
+def task_queues(hmb: int, frames: int):
+    """-> (the launch's tasks partitioned into per-label queues: int32 (frame
+    << 16 | row), the 9 segment bounds, the number of labels)."""
+    out = np.zeros(frames * hmb, np.int32)
+    seg = np.zeros(9, np.int32)
+    nlab = ctypes.c_int()
+    _ck(lib().cairo_task_queues(hmb, frames, _ptr(out), _ptr(seg), ctypes.byref(nlab)), "cairo_task_queues")
+    return out, seg, nlab.value
 
 
 def serialize_slice(table: np.ndarray, wmb: int, hmb: int, ring: int, cy, cu, cv, capacity_bytes: int | None = None):

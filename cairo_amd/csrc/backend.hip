@@ -122,7 +122,8 @@ struct cairo_ctx {
   hipEvent_t batch_ready[kSyncAreas] = {};  // its frames converted, views and sync area set up
   // the last launch, whose remaining tasks the next launch's workers take first
   const FrameArgs* prev_fa = nullptr;
-  const int32_t* prev_order = nullptr;
+  const int32_t* prev_order[2] = {};
+  const int32_t* prev_seg[2] = {};
   int32_t* prev_sync = nullptr;
   int prev_total = 0, prev_area = 0, prev_decode = 0;
   int order_slope = kOrderSlope;  // of the task order tables (3N + 2 in an N-member group)
@@ -284,7 +285,6 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.sync = c->sync;
   e.sticky = c->sticky;
   e.stamps = c->stamps;
-  e.order = c->order;
   e.trace = c->trace_dev;
   return e;
 }
@@ -324,6 +324,48 @@ std::vector<int32_t> task_order(int hmb, int slope) {
       }
   }
   return ord;
+}
+
+// The device block of task orders (OrderBlock): for every batch size the
+// plain order (one queue per pool) and the labelled one (task_order stably
+// partitioned by task_label: one queue per label and pool), then each one's
+// label segments.
+struct OrderBlock {
+  static size_t order_at(int hmb, int banded, int nf) { return ((size_t)banded * kMaxBatch + nf - 1) * kMaxBatch * hmb; }
+  static size_t seg_at(int hmb, int banded, int nf) {
+    return (size_t)2 * kMaxBatch * kMaxBatch * hmb + ((size_t)banded * kMaxBatch + nf - 1) * (kLabels + 1);
+  }
+  static size_t words(int hmb) { return seg_at(hmb, 2, 1); }
+};
+
+std::vector<int32_t> order_block(int hmb, int slope) {
+  const std::vector<int32_t> ord = task_order(hmb, slope);
+  std::vector<int32_t> blk(OrderBlock::words(hmb), 0);
+  for (int nf = 1; nf <= kMaxBatch; nf++) {
+    const int32_t* o = &ord[(size_t)(nf - 1) * kMaxBatch * hmb];
+    const int total = nf * hmb;
+    std::copy(o, o + total, &blk[OrderBlock::order_at(hmb, 0, nf)]);
+    int32_t* seg = &blk[OrderBlock::seg_at(hmb, 0, nf)];
+    for (int l = 1; l <= kLabels; l++) seg[l] = total;
+    int32_t* ob = &blk[OrderBlock::order_at(hmb, 1, nf)];
+    int32_t* sb = &blk[OrderBlock::seg_at(hmb, 1, nf)];
+    int n = 0;
+    for (int l = 0; l < kLabels; l++) {
+      sb[l] = n;
+      for (int i = 0; i < total; i++)
+        if (task_label(o[i] >> 16, o[i] & 0xFFFF, hmb) == l) ob[n++] = o[i];
+    }
+    sb[kLabels] = n;
+  }
+  return blk;
+}
+
+int upload_orders(cairo_ctx* c, int slope) {
+  c->order_slope = slope;
+  const std::vector<int32_t> blk = order_block((int)c->hmb, slope);
+  CK(hipMemcpy(c->order, blk.data(), blk.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->prev_total = 0;  // the previous launch's queue used the other order
+  return kSuccess;
 }
 
 void free_ctx(cairo_ctx* c) {
@@ -434,7 +476,6 @@ int flush(cairo_ctx* c) {
   CK(hipSetDevice(c->device));
   EngineArgs e = engine_args(c);
   e.nframes = c->npend;
-  e.order = c->order + (size_t)(e.nframes - 1) * kMaxBatch * c->hmb;
   // frame descriptors -> device (a ring of pinned slots: the copy of an earlier
   // launch may still be pending when this one is written)
   const int fslot = c->fdesc_next;
@@ -464,7 +505,7 @@ int flush(cairo_ctx* c) {
   const int area = (int)(b % kSyncAreas);
   e.sync = c->sync + (size_t)area * c->sync_words;
   e.pfa = c->prev_fa;
-  e.porder = c->prev_order;
+  for (int k = 0; k < 2; k++) e.porder[k] = c->prev_order[k], e.pseg[k] = c->prev_seg[k];
   e.psync = c->prev_sync;
   e.ptotal = c->prev_decode == e.decode ? c->prev_total : 0;  // a worker runs one kind of task
   e.slope = c->order_slope;
@@ -475,6 +516,15 @@ int flush(cairo_ctx* c) {
     int nr = total - nh;
     e.n_helpers = std::max(1, std::min(nh, rows));
     e.n_rows = std::max(1, std::min(nr, rows));
+  }
+  // XCD-banded queues (kernels.h kLabels) on large frames, when both pools
+  // split evenly over the labels
+  const int banded = c->hmb >= (uint32_t)kBandMinRows && e.n_helpers % kLabels == 0 && e.n_rows % kLabels == 0;
+  for (int k = 0; k < 2; k++) {
+    const int bk = banded && (kBandPools >> k & 1);
+    e.nlab[k] = bk ? kLabels : 1;
+    e.order[k] = c->order + OrderBlock::order_at((int)c->hmb, bk, e.nframes);
+    e.seg[k] = c->order + OrderBlock::seg_at((int)c->hmb, bk, e.nframes);
   }
   // this sync area was last used by launch b-3 (only a launch reads its own
   // area); launch b-2 precedes this one on the same stream
@@ -522,7 +572,7 @@ int flush(cairo_ctx* c) {
   // when every task has finished (the next launch's workers may run the last)
   CK(launch_batch_wait(e.sync, 2 * rows, c->sticky, st));
   c->prev_fa = fd;
-  c->prev_order = e.order;
+  for (int k = 0; k < 2; k++) c->prev_order[k] = e.order[k], c->prev_seg[k] = e.seg[k];
   c->prev_sync = e.sync;
   c->prev_total = rows;
   c->prev_area = area;
@@ -739,11 +789,14 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
   {  // (frame, row) task order of the engine pools, for every batch size
-    const std::vector<int32_t> ord = task_order((int)c->hmb, kOrderSlope);
     TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch, hipHostMallocDefault));
     TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch));
-    TRY(hipMalloc(&c->order, ord.size() * sizeof(int32_t)));
-    TRY(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    TRY(hipMalloc(&c->order, OrderBlock::words((int)c->hmb) * sizeof(int32_t)));
+    r = upload_orders(c, kOrderSlope);
+    if (r != kSuccess) {
+      free_ctx(c);
+      return r;
+    }
   }
   for (auto& s : c->st) {
     TRY(hipHostMalloc(&s.table, c->mbs * sizeof(BlockDesc), hipHostMallocDefault));
@@ -783,9 +836,8 @@ int cairo_ctx_reset(cairo_ctx* c) {
   for (auto& s : c->st) s.busy = false;
   if (c->gsize > 1) {  // a reset leaves the group (its members reset and rejoin together)
     leave_group(c);
-    c->order_slope = kOrderSlope;
-    const std::vector<int32_t> ord = task_order((int)c->hmb, kOrderSlope);
-    CK(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    r = upload_orders(c, kOrderSlope);
+    if (r) return r;
   }
   return zero_state(c);
 }
@@ -802,6 +854,16 @@ int cairo_task_order(int hmb, int frames, int32_t* out, int* slope) {
   const std::vector<int32_t> ord = task_order(hmb, kOrderSlope);
   memcpy(out, &ord[(size_t)(frames - 1) * kMaxBatch * hmb], (size_t)frames * hmb * sizeof(int32_t));
   if (slope) *slope = kOrderSlope;
+  return kSuccess;
+}
+
+int cairo_task_queues(int hmb, int frames, int32_t* order, int32_t* seg, int* nlab) {
+  if (hmb < 1 || hmb > 0xFFFF || frames < 1 || frames > kMaxBatch || !order || !seg) return kInvalidArg;
+  const std::vector<int32_t> blk = order_block(hmb, kOrderSlope);
+  const int banded = hmb >= kBandMinRows;
+  memcpy(order, &blk[OrderBlock::order_at(hmb, banded, frames)], (size_t)frames * hmb * sizeof(int32_t));
+  memcpy(seg, &blk[OrderBlock::seg_at(hmb, banded, frames)], (kLabels + 1) * sizeof(int32_t));
+  if (nlab) *nlab = banded ? kLabels : 1;
   return kSuccess;
 }
 
@@ -1302,11 +1364,7 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
   CK(hipMalloc(&c->zero, c->plane_elems * 2));
   CK(hipMemset(c->zero, 0, c->plane_elems * 2));
   // a member's consecutive frames are N stream frames apart
-  c->order_slope = 3 * size + 2;
-  const std::vector<int32_t> ord = task_order((int)c->hmb, c->order_slope);
-  CK(hipMemcpy(c->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  c->prev_total = 0;  // the previous launch's queue used the other order
-  return kSuccess;
+  return upload_orders(c, 3 * size + 2);
 }
 
 int cairo_ctx_release(cairo_ctx* c, int ticket) {

@@ -153,10 +153,11 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j);
 // launch itself).  ng = inter-search groups per MB row ((wmb + 3) / 4).
 struct SyncLayout {
   static constexpr int kErr = 0;
-  static constexpr int kTicketRows = 2;
-  static constexpr int kTicketHelpers = 3;
   static constexpr int kDone = 4;  // finished tasks (helpers + coders) of the batch
-  static constexpr int kFlags = 8;
+  static constexpr int kLabelOff = 5;  // 1 + the label offset the launch's workers agreed on (0: not yet)
+  static constexpr int kTicketRows = 8;      // + label: next ticket of each label's coder queue
+  static constexpr int kTicketHelpers = 16;  // + label: of each label's helper queue
+  static constexpr int kFlags = 24;
   // per frame j: inter_done[hmb][ng] (tasks finished per group)
   __host__ __device__ static int frame_words(int hmb, int ng) { return hmb * ng; }
   __host__ __device__ static int inter_done(int hmb, int ng, int j) { return kFlags + frame_words(hmb, ng) * j; }
@@ -180,14 +181,20 @@ struct EngineArgs {
   uint64_t* stamps;
   int n_helpers, n_rows;   // worker pools (workgroups), spread over the block indices (is_helper)
   int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)
-  const int32_t* order;    // [nframes * hmb] task order of every pool: (frame << 16 | row),
-                           // sorted by (row + kOrderSlope * frame, frame)
+  // Per pool (0 helpers, 1 row coders): [nframes * hmb] task order, (frame << 16 | row)
+  // sorted by (row + kOrderSlope * frame, frame), then stably partitioned by label
+  // (nlab == kLabels); label l's queue is order[seg[l] .. seg[l+1]).
+  const int32_t* order[2];
+  const int32_t* seg[2];   // [kLabels + 1] each
+  int nlab[2];             // 1, or kLabels: one queue per XCD (label = XCD when the dispatcher
+                           // deals blocks round-robin; see task_label)
   int decode;              // the launch decodes (every frame has FrameDesc::decode set)
   // The previous launch (still running, or done): its remaining tasks come
   // first for this launch's workers too, so the two co-resident launches
   // share their pools (ptotal = 0: none).
   const FrameArgs* pfa;
-  const int32_t* porder;
+  const int32_t* porder[2];
+  const int32_t* pseg[2];
   int32_t* psync;
   int ptotal;
   int slope;               // of both task orders (kOrderSlope; 3N + 2 for a member of an N-GPU group)
@@ -201,6 +208,39 @@ struct EngineArgs {
 #define CAIRO_ORDER_SLOPE 5
 #endif
 constexpr int kOrderSlope = CAIRO_ORDER_SLOPE;
+
+// XCD-banded queues: on a frame of at least kBandMinRows macroblock rows each
+// pool keeps one queue per label (kLabels), and a worker serves the queue of
+// its label (kernels.hip next_task: unless another label's head is more than
+// kSteal keys earlier): the workgroups b with one value of b % 8 share an XCD
+// (the observed round-robin deal), and the launch agrees on one offset so
+// that a label is an XCD.  Row r of every frame has label r * kLabels / hmb
+// (contiguous bands): the helpers of neighbouring rows, whose search windows
+// overlap by 64 of 80 lines, and the coders of the rows they feed share an
+// L2.  Correctness does not rest on the placement: labels partition the block
+// indices, each label has workers of both pools, and each label's queue is a
+// subsequence of the task order (deadlock freedom as for one queue).
+// 4K A/B: 5387-5391 -> 5483-5486 Mpix/s, engine reads -29 %;
+// at 1080p (68 rows) -1.2 %, so not below kBandMinRows.
+constexpr int kLabels = 8;
+#ifndef CAIRO_BAND_MIN_ROWS
+#define CAIRO_BAND_MIN_ROWS 100
+#endif
+constexpr int kBandMinRows = CAIRO_BAND_MIN_ROWS;
+#ifndef CAIRO_BAND_POOLS
+#define CAIRO_BAND_POOLS 3  // bit 0: the helpers' queues are per label, bit 1: the coders'
+#endif
+constexpr int kBandPools = CAIRO_BAND_POOLS;
+#ifndef CAIRO_BAND_SHIFT
+#define CAIRO_BAND_SHIFT -1  // < 0: contiguous bands of hmb / kLabels rows
+#endif
+#ifndef CAIRO_BAND_ROT
+#define CAIRO_BAND_ROT 5
+#endif
+__host__ __device__ inline int task_label(int frame, int row, int hmb) {
+  if (CAIRO_BAND_SHIFT < 0) return row * kLabels / hmb;
+  return ((row >> (CAIRO_BAND_SHIFT < 0 ? 0 : CAIRO_BAND_SHIFT)) + frame * CAIRO_BAND_ROT) & (kLabels - 1);
+}
 
 // RGB -> YUV of every frame of the batch into its slot's source planes.
 hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);

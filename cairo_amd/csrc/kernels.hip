@@ -2308,7 +2308,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 // ---------------------------------------------------------------------------
 // The engine: one persistent launch encodes a batch of consecutive frames,
 // pipelined across frames.  Two worker pools (helpers and row coders,
-// spread over the block indices: is_helper) dequeue (frame, row) tasks in e.order (by row + slope * frame):
+// spread over the block indices: is_helper) dequeue (frame, row) tasks in their e.order (by row + slope * frame):
 //   helper (j, r): inter search of row r, group g (MBs 4g..4g+3) once the
 //           previous frame is final on MB rows r-2..r+2 over the group's
 //           search window [64g-32, 64g+96) (this also covers every older
@@ -2341,44 +2341,117 @@ __device__ __forceinline__ bool is_helper(int b, int nh, int n) {
   return ((b + 1) * nh) / n > (b * nh) / n;
 }
 
-// The next task of a pool (ticket word tk): from this launch's queue or the
-// previous launch's, whichever task comes first in the task order (row +
-// e.slope * frame; the previous launch's frames come first, so its frame
-// j is this launch's frame j - pframes).  The previous batch's tail thereby
-// interleaves with this batch's first rows as the order says, and every free
-// worker of either launch takes the oldest task: the two co-resident launches
-// share their pools.  Returns the ticket (prev: of the previous launch), or
-// -1 when both queues are exhausted.
+// The next task of a pool.  Each label has a queue in the task order (row +
+// e.slope * frame) in this launch and one in the previous launch's (whose
+// frames come first, so its frame j is this launch's frame j - pframes); a
+// label's head is the earlier of the two, so the previous batch's tail
+// interleaves with this batch's first rows as the order says and the two
+// co-resident launches share their pools.  A worker takes its own label's
+// head unless another label's head is more than kSteal keys earlier (or its
+// own queues are exhausted): then it takes that one.  Every task a worker
+// takes is thus no later than its own label's head, so the oldest unfinished
+// task always has a free worker: its label's workers hold only
+// finished tasks.  Returns the task's index in its order (prev: the previous
+// launch's), or -1 when every queue is exhausted.
 #ifndef CAIRO_SHARE
 #define CAIRO_SHARE 1
 #endif
-__device__ __forceinline__ int next_task(const EngineArgs& e, int tk, int total, EngineLds& L, bool& prev) {
+#ifndef CAIRO_STEAL
+#define CAIRO_STEAL 2
+#endif
+constexpr int kSteal = CAIRO_STEAL;
+__device__ __forceinline__ int next_task(const EngineArgs& e, int pool, int lab, EngineLds& L, bool& prev) {
   const int ptotal = CAIRO_SHARE ? e.ptotal : 0;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // wave 0; lane l < nlab looks after label l
+    const int l = threadIdx.x, nlab = e.nlab[pool];
+    const bool act = l < nlab;
     const int pframes = ptotal / e.hmb;
-    int q = 0, tt = -1;
-    for (;;) {
-      const int tp = ptotal ? __hip_atomic_load(e.psync + tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      const int tb = __hip_atomic_load(e.sync + tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tp >= ptotal && tb >= total) break;  // both exhausted
-      bool usep = tp < ptotal;
-      if (usep && tb < total) {
-        const int op = e.porder[tp], ob = e.order[tb];
-        usep = (op & 0xFFFF) + e.slope * (op >> 16) <= (ob & 0xFFFF) + e.slope * (pframes + (ob >> 16));
-      }
-      tt = __hip_atomic_fetch_add((usep ? e.psync : e.sync) + tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      q = usep;
-      if (tt < (usep ? ptotal : total)) break;  // else taken meanwhile: look again
-      tt = -1;
+    const int tk = (pool ? SyncLayout::kTicketRows : SyncLayout::kTicketHelpers) + (act ? l : 0);
+    const int32_t* __restrict__ order = e.order[pool];
+    const int32_t* __restrict__ porder = e.porder[pool];
+    int b0 = 0, n0 = 0, pb0 = 0, pn0 = 0;
+    if (act) {
+      b0 = e.seg[pool][l], n0 = e.seg[pool][l + 1] - b0;
+      if (ptotal) pb0 = e.pseg[pool][l], pn0 = e.pseg[pool][l + 1] - pb0;
     }
-    L.slot = tt;
-    L.flag = q;
+    constexpr int kNone = 0x7FFFFFFF;
+    int res = -1, q = 0;
+    for (;;) {
+      int key = kNone;
+      bool usep = false;
+      if (act) {
+        const int tp = pn0 ? __hip_atomic_load(e.psync + tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        const int tb = __hip_atomic_load(e.sync + tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int kp = kNone, kb = kNone;
+        if (tp < pn0) {
+          const int op = porder[pb0 + tp];
+          kp = (op & 0xFFFF) + e.slope * (op >> 16);
+        }
+        if (tb < n0) {
+          const int ob = order[b0 + tb];
+          kb = (ob & 0xFFFF) + e.slope * (pframes + (ob >> 16));
+        }
+        usep = kp <= kb && kp != kNone;
+        key = min(kp, kb);
+      }
+      int mn = key;
+      for (int o = 1; o < kLabels; o <<= 1) mn = min(mn, __shfl_xor(mn, o));
+      mn = __shfl(mn, 0);
+      if (mn == kNone) break;  // every queue exhausted
+      const int own = __shfl(key, lab);
+      const int z = (own != kNone && own - mn <= kSteal) ? lab : __ffsll(__ballot(act && key == mn)) - 1;
+      int ok = 0;
+      if (l == z) {
+        const int tt = __hip_atomic_fetch_add((usep ? e.psync : e.sync) + tk, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        if (tt < (usep ? pn0 : n0)) ok = 1, res = tt + (usep ? pb0 : b0), q = usep;
+      }
+      if (__shfl(ok, z)) {  // else taken meanwhile: look again
+        res = __shfl(res, z), q = __shfl(q, z);
+        break;
+      }
+    }
+    if (l == 0) {
+      L.slot = res;
+      L.flag = q;
+    }
   }
   __syncthreads();
   const int t = uni(L.slot);
   prev = uni(L.flag) != 0;
   __syncthreads();
   return t;
+}
+
+// This workgroup's label and pool.  With per-label queues (e.nlab ==
+// kLabels) the block indices split into kLabels classes (b % kLabels), each
+// with its share of both pools; the launch's workers agree on one offset
+// (the first to arrive proposes XCC_ID - b, i.e. the offset that makes a
+// label an XCD when blocks are dealt round-robin) so labels stay a
+// partition of the classes whatever the placement.
+#ifndef CAIRO_CLASS_SPLIT
+#define CAIRO_CLASS_SPLIT 0
+#endif
+__device__ __forceinline__ int worker_label(const EngineArgs& e, int b, bool& helper, EngineLds& L) {
+  const int n = e.n_helpers + e.n_rows;
+  if (e.nlab[0] == 1 && e.nlab[1] == 1 && !(CAIRO_CLASS_SPLIT && n % kLabels == 0 && e.n_helpers % kLabels == 0)) {
+    helper = is_helper(b, e.n_helpers, n);
+    return 0;
+  }
+  helper = is_helper(b / kLabels, e.n_helpers / kLabels, n / kLabels);
+  if (e.nlab[helper ? 0 : 1] == 1) return 0;
+  if (threadIdx.x == 0) {
+    const int xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kLabels - 1);  // HW_REG_XCC_ID[3:0]
+    int want = ((xcc - b) & (kLabels - 1)) + 1, seen = 0;
+    if (!__hip_atomic_compare_exchange_strong(e.sync + SyncLayout::kLabelOff, &seen, want, __ATOMIC_RELAXED,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      want = seen;
+    L.slot = (b + want - 1) & (kLabels - 1);
+  }
+  __syncthreads();
+  const int lab = uni(L.slot);
+  __syncthreads();
+  return lab;
 }
 
 // A finished task counts toward its batch's completion (k_batch_wait) once
@@ -2401,18 +2474,19 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   uint64_t* ks = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, hmb) : nullptr;
   if (ks && threadIdx.x == 0)
     __hip_atomic_fetch_min(&ks[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int total = e.nframes * hmb;
-  if (is_helper(b, e.n_helpers, e.n_helpers + e.n_rows)) {
+  bool helper;
+  const int lab = worker_label(e, b, helper, L);
+  if (helper) {
     // The helpers' inter records gate every row coder at its group starts:
     // on large frames they win the SIMD issue arbitration against the coders'
     // waves (A/B: 1080p +3 %, 4K +3 %; 720p -1 %, so not there).
     if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(CAIRO_PRIO_LEVEL);
     for (;;) {
       bool prev;
-      const int t = next_task(e, SyncLayout::kTicketHelpers, total, L, prev);
+      const int t = next_task(e, 0, lab, L, prev);
       if (t < 0) break;
       trace(e.trace, 0, 1000000 + t);
-      const int32_t o = (prev ? e.porder : e.order)[t];
+      const int32_t o = (prev ? e.porder : e.order)[0][t];
       row_helper(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.helper, &L.flag, e.trace);
       task_done(prev ? e.psync : e.sync);
       trace(e.trace, 0, 2000000 + t);
@@ -2420,10 +2494,10 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
   } else {
     for (;;) {
       bool prev;
-      const int t = next_task(e, SyncLayout::kTicketRows, total, L, prev);
+      const int t = next_task(e, 1, lab, L, prev);
       if (t < 0) break;
       trace(e.trace, 0, 3000000 + t);
-      const int32_t o = (prev ? e.porder : e.order)[t];
+      const int32_t o = (prev ? e.porder : e.order)[1][t];
       code_row<kDecode>(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.row, &L.flag, e.trace);
       task_done(prev ? e.psync : e.sync);
       trace(e.trace, 0, 4000000 + t);

@@ -111,6 +111,12 @@ CAIRO_API int cairo_default_batch(uint32_t width, uint32_t height);
  * previous launch's tasks, merged by the same key with that launch's frames
  * first (no device needed; for tests of the deadlock-freedom argument). */
 CAIRO_API int cairo_task_order(int hmb, int frames, int32_t *out, int *slope);
+/* The per-label queues of a launch of one context (kernels.h kLabels): the
+ * same tasks as cairo_task_order, stably partitioned by label, label l's queue
+ * being order[seg[l] .. seg[l+1]) (seg: 9 words); *nlab receives 8 on frames
+ * of at least 100 macroblock rows (one queue per XCD and pool), else 1 (seg =
+ * {0, total, ...}).  No device needed. */
+CAIRO_API int cairo_task_queues(int hmb, int frames, int32_t *order, int32_t *seg, int *nlab);
 
 /* Introspection (synchronous; of the last submitted frame).  which: 0 input,
  * 1 output_cache, 2+k ring slot k. */

@@ -89,3 +89,82 @@ def test_task_order_rejects_bad_sizes(cairo):
         cairo.task_order(0, 1)
     with pytest.raises(cairo.CairoError):
         cairo.task_order(10, 33)
+
+
+@pytest.mark.parametrize("hmb", [3, 18, 45, 68, 99, 100, 135, 270])
+def test_label_queues_partition_the_order(cairo, hmb):
+    """XCD-banded queues (kernels.h kLabels): each label's queue is the
+    launch's task order restricted to that label's rows, a contiguous band."""
+    for frames in (1, 2, 7, 28, 32):
+        o, slope = cairo.task_order(hmb, frames)
+        q, seg, nlab = cairo.task_queues(hmb, frames)
+        assert nlab == (8 if hmb >= 100 else 1)
+        assert seg[0] == 0 and list(seg) == sorted(seg) and seg[nlab] == frames * hmb
+        assert all(seg[l] == frames * hmb for l in range(nlab, 9))
+        lab_of = lambda x: (int(x) & 0xFFFF) * 8 // hmb if nlab == 8 else 0
+        for lab in range(nlab):
+            mine = list(q[seg[lab]:seg[lab + 1]])
+            assert mine == [x for x in o if lab_of(x) == lab]
+        if nlab == 8:  # contiguous bands, every label has rows
+            bands = [sorted({int(x) & 0xFFFF for x in q[seg[l]:seg[l + 1]]}) for l in range(8)]
+            assert all(b and b == list(range(b[0], b[-1] + 1)) for b in bands)
+
+
+def _simulate(queues, workers, deps, key, steal=None):
+    """Per-label worker pools taking their label's queue in order (with
+    steal = W: another label's head instead when it is more than W keys
+    earlier, or when the own queue is exhausted: kernels.hip next_task); a
+    task finishes once everything it waits for has finished.  -> finished
+    count."""
+    done, heads = set(), [0] * len(queues)
+    held = [[None] * workers for _ in queues]
+    total = sum(len(q) for q in queues)
+    inf = float("inf")
+
+    def take(lab):
+        ks = [key(q[heads[l]]) if heads[l] < len(q) else inf for l, q in enumerate(queues)]
+        if min(ks) == inf:
+            return None
+        z = lab
+        if steal is not None and (ks[lab] == inf or ks[lab] - min(ks) > steal):
+            z = ks.index(min(ks))
+        if ks[z] == inf:
+            return None
+        heads[z] += 1
+        return queues[z][heads[z] - 1]
+
+    while len(done) < total:
+        moved = False
+        for lab in range(len(queues)):
+            for w in range(workers):
+                t = held[lab][w]
+                if t is None:
+                    t = held[lab][w] = take(lab)
+                    moved |= t is not None
+                if t is not None and all(d in done for d in deps(t)):
+                    done.add(t)
+                    held[lab][w] = None
+                    moved = True
+        if not moved:
+            break
+    return len(done)
+
+
+@pytest.mark.parametrize("hmb", [100, 135])
+@pytest.mark.parametrize("steal", [None, 0, 2, 7])
+def test_label_queues_cannot_deadlock(cairo, hmb, steal):
+    """Two consecutive launches, every label merging the previous launch's
+    queue with its own (next_task), with or without stealing: with a single
+    worker per label every task still finishes, whatever the label of the
+    rows it waits for."""
+    n1, n2 = 5, 3
+    p, seg1, _ = cairo.task_queues(hmb, n1)
+    c, seg2, _ = cairo.task_queues(hmb, n2)
+    _, slope = cairo.task_order(hmb, 1)
+    queues = []
+    for lab in range(8):
+        # every label has rows of every frame, so _merge numbers the second
+        # launch's frames from n1, as next_task does (ptotal / hmb)
+        queues.append(_merge(p[seg1[lab]:seg1[lab + 1]], c[seg2[lab]:seg2[lab + 1]], slope))
+    n = _simulate(queues, 1, lambda t: _deps(t[0], t[1], hmb), lambda t: t[1] + slope * t[0], steal)
+    assert n == (n1 + n2) * hmb
