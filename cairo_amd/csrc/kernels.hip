@@ -203,6 +203,11 @@ __device__ __forceinline__ void acquire_fence(bool sys) {
 #ifndef CAIRO_GRAN_SLEEP
 #define CAIRO_GRAN_SLEEP 1
 #endif
+// Deblock readiness (and the helper's progress poll): the words tested loaded together (1) or one after
+// the other (0).
+#ifndef CAIRO_READY_PAIR
+#define CAIRO_READY_PAIR 1
+#endif
 
 // Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
 // timeout (~2 s) the error word is set and the wait gives up, so every
@@ -761,10 +766,19 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
-      if (!pp || progress_peer(a.sys, pp + rr) >= tagged(a.epoch - back, need)) {
+#if CAIRO_READY_PAIR
+      // the progress poll and the deblock readiness loads in flight together
+      const uint64_t pv = pp ? progress_peer(a.sys, pp + rr) : ~0ull;
+      const bool dbr = kDeblock && !kCoderDeblock && kHelperInterleave && deblock_pending(a, st) &&
+                       deblock_chunk_ready(a, r, st);
+#else
+      const uint64_t pv = pp ? progress_peer(a.sys, pp + rr) : ~0ull;
+      const bool dbr = pv < tagged(a.epoch - back, need) && kDeblock && !kCoderDeblock && kHelperInterleave &&
+                       deblock_pending(a, st) && deblock_chunk_ready(a, r, st);
+#endif
+      if (pv >= tagged(a.epoch - back, need)) {
         d = 1;
-      } else if (kDeblock && !kCoderDeblock && kHelperInterleave && deblock_pending(a, st) &&
-                 deblock_chunk_ready(a, r, st)) {
+      } else if (dbr) {
         d = 2;
       } else {  // nothing to do: back off
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -1290,6 +1304,11 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 constexpr int kDbChunk = 64;  // the widest chunk: luma columns (tile width, info table, arrays)
 constexpr int kDbMBs = kDbChunk / 16;
 __device__ __forceinline__ int db_chunks(const FA& a) { return (a.wa + (1 << a.db_shift) - 1) >> a.db_shift; }
+// The filters of a 64-column chunk over all four waves (1) or in wave 0 (0).
+#ifndef CAIRO_DB_SPREAD
+#define CAIRO_DB_SPREAD 1
+#endif
+constexpr bool kDbSpread = CAIRO_DB_SPREAD;
 constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
 constexpr int kDbCW = 64, kDbCP = 66;    // chroma
 
@@ -1350,10 +1369,18 @@ __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st) {
 
 __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState& st) {
   const int c1 = min((st.k + 1) << a.db_shift, a.wa);
+  // Row r-1's progress and the info granule of the chunk's last macroblock
+  // (stored last; the row is coded left to right), both loads issued before
+  // either is tested: one fabric round trip, not two.
+#if CAIRO_READY_PAIR
+  const uint64_t p = r > 0 ? progress_at(&a.progress[r - 1]) : ~0ull;
+  const uint64_t g = gran_ld(gran_mb(a, (c1 - 1) >> 4, r) + kGranulesPerMB);
+  return (p >= tagged(a.epoch, c1)) & ((uint32_t)(g >> 32) == a.epoch);
+#else
   if (r > 0 && progress_at(&a.progress[r - 1]) < tagged(a.epoch, c1)) return false;
-  // the info granule of the chunk's last macroblock (stored last; the row is coded left to right)
   const uint64_t g = gran_ld(gran_mb(a, (c1 - 1) >> 4, r) + kGranulesPerMB);
   return (uint32_t)(g >> 32) == a.epoch;
+#endif
 }
 
 // Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs, or
@@ -1455,13 +1482,19 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
     }
     __syncthreads();
     const uint64_t t1 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
-    // ---- the filters, in order, by wave 0 alone: a wave's LDS accesses
-    //      execute in order, so no workgroup barrier between the steps ----
-    if (tid < 64) {
-      const int lane = tid;
+    // ---- the filters, in four dependent phases (band A H edges, band A V
+    //      edges, band B H, band B V); the lines of one phase are disjoint.
+    //      64-column chunks (4K) spread each phase over the four waves with a
+    //      workgroup barrier between phases; narrower chunks have at most 64
+    //      lines per phase and stay in wave 0, whose LDS accesses execute in
+    //      order (no workgroup barrier) ----
+    {
+      const bool spread = kDbSpread && a.db_shift >= 6;  // workgroup-uniform
+      const int nthr = spread ? 256 : 64;
+      const bool part = tid < nthr;
       const int ls = a.db_shift, kL = 1 << ls, kC = kL >> 1;  // luma / chroma columns of a whole chunk
       // band A H edges of [c0, c1): luma kL columns, then chroma 2 x kC
-      for (int i = lane; r > 0 && i < kL + 2 * kC; i += 64) {
+      for (int i = tid; part && r > 0 && i < kL + 2 * kC; i += nthr) {
         if (i < kL) {
           const int col = c0 + i;
           if (col < c1) db_line(D, 0, true, 0, col, D.info[0][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
@@ -1471,9 +1504,9 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
             db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      if (spread) __syncthreads(); else __builtin_amdgcn_wave_barrier();
       // band A V edges of the luma units c0, c0+8, ... and the chroma units c0/2, c0/2+8, ...
-      for (int i = lane; i < kL + 2 * kC; i += 64) {
+      for (int i = tid; part && i < kL + 2 * kC; i += nthr) {
         if (i < kL) {
           const int x = c0 + 8 * (i >> 3), row = 4 + (i & 7);
           if (x > 0 && x < c1)
@@ -1484,12 +1517,12 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
             db_line(D, pl, false, row, x - 4, D.info[1][((x - 1) >> 3) & 7], D.info[1][(x >> 3) & 7]);
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      if (spread) __syncthreads(); else __builtin_amdgcn_wave_barrier();
       // band B H edges of [hb0, hb1), then V edges of units [vb0, vb1)
-      for (int col = hb0 + lane; col < hb1; col += 64)
+      for (int col = hb0 + tid; part && col < hb1; col += nthr)
         db_line(D, 0, true, 8, col, D.info[1][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
-      __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < 8 * ((vb1 - vb0 + 7) >> 3); i += 64) {
+      if (spread) __syncthreads(); else __builtin_amdgcn_wave_barrier();
+      for (int i = tid; part && i < 8 * ((vb1 - vb0 + 7) >> 3); i += nthr) {
         const int x = vb0 + 8 * (i >> 3), row = 12 + (i & 7);
         if (x < vb1) db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
       }
@@ -1621,8 +1654,9 @@ __device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbSt
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
-      const bool recs = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.nref;
+      const int nrec = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool can = ((st.k + 1) << (a.db_shift - 4)) <= bx && deblock_chunk_ready(a, by, st);
+      const bool recs = nrec >= a.nref;
       if (can && (!recs || (bx >> (a.db_shift - 4)) - st.k > kCoderDbLag)) {
         d = 2;
       } else if (recs || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
