@@ -8,10 +8,15 @@ Per quality q, on the band4 content (seed 1234), ring R = 4:
     entropy), plus the 10-byte frame descriptor the encoder writes per frame;
   * distortion: PSNR (peak 255) of the last frame's deblocked reconstruction
     against its converted source, luma and chroma separately.
+  * a pin: the canonical SHA-256 (tail bits and header byte 7 masked) of the
+    stream records of frames 0..--check-1 as the pipeline produced them, so
+    that tests/test_rd_sweep_pinned.py can compare the committed table with the
+    oracle on the CPU (this tool itself never loads the oracle).
 Writes one JSON object per q to stdout and the whole table to --out.
 usage (GPU box): python tools/rd_sweep.py [--config 4k] [--frames 48] [--q 1,4,8,...]
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -31,12 +36,27 @@ def psnr(a, b):
     return float("inf") if mse == 0 else 10.0 * math.log10(255.0 ** 2 / mse)
 
 
+def record_sha(w, h, ring, q, t, payload, nbits):
+    """Canonical SHA-256 (16 hex digits) of frame t's stream record: header or
+    descriptor + payload, bits beyond the end and header byte 7 zeroed."""
+    import cairo_amd
+
+    rec, n = bench.record(cairo_amd, w, h, ring, q, t, payload, nbits)
+    b = bytearray(rec[: (n + 7) // 8])
+    if n % 8:
+        b[-1] &= (1 << (n % 8)) - 1
+    if t == 0 and len(b) > 7:
+        b[7] = 0
+    return hashlib.sha256(bytes(b)).hexdigest()[:16], n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="4k", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=160, help="timed P-frames per quality")
     ap.add_argument("--q", default="1,2,4,8,12,16,20,24,28,31")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rd_sweep.json"))
+    ap.add_argument("--check", type=int, default=3, help="frames per quality pinned by their record hashes")
     a = ap.parse_args()
     import torch
 
@@ -73,12 +93,22 @@ def main():
         st = cairo_amd.Stream(ctx, threads=14)
         tks = []
         bits = []
+        pins = []
+
+        def take(tk):
+            data, nb = st.collect(tk)
+            t = len(bits)
+            bits.append(nb)
+            if t < a.check:
+                sha, rec_bits = record_sha(w, h, ring, q, t, data, nb)
+                pins.append({"frame": t, "record_bits": rec_bits, "sha256_16": sha})
+
         for f in range(n):
             tks.append(st.submit(ptr(f), f, f > 0, q, on_device=True))
             if len(tks) == stages:
-                bits.append(st.collect(tks.pop(0))[1])
+                take(tks.pop(0))
         while tks:
-            bits.append(st.collect(tks.pop(0))[1])
+            take(tks.pop(0))
         st.close()
         last = n - 1
         src = ctx.read_planes(0)
@@ -92,7 +122,8 @@ def main():
                "i_frame_kbytes": round((bits[0] / 8 + 24) / 1e3, 2),
                "psnr_y": round(psnr(src[0][:hh, :ww], rec[0][:hh, :ww]), 2),
                "psnr_u": round(psnr(src[1][:hh // 2, :ww // 2], rec[1][:hh // 2, :ww // 2]), 2),
-               "psnr_v": round(psnr(src[2][:hh // 2, :ww // 2], rec[2][:hh // 2, :ww // 2]), 2)}
+               "psnr_v": round(psnr(src[2][:hh // 2, :ww // 2], rec[2][:hh // 2, :ww // 2]), 2),
+               "pinned_frames": pins}
         rows.append(row)
         print(json.dumps(row), flush=True)
     out = {"config": f"{w}x{h} p-frames, ring R={ring}, band4 seed 1234 (BASELINE.json configs[4])",
