@@ -936,8 +936,15 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     const int back = off == 1 ? 1 : 2;
     const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
     const uint64_t want = tagged(a.epoch - back, inter_need_cols(a, g, 2));
+#if CAIRO_READY_PAIR
+    // both words loaded before either is tested (one round trip)
+    const uint64_t w3 = pp ? progress_peer(a.sys, pp + min(r + 3, a.hmb - 1)) : 0;
+    const uint64_t w2 = pp ? progress_peer(a.sys, pp + min(r + 2, a.hmb - 1)) : 0;
+    const int full = !pp || ((w3 >= want) & (w2 >= want));
+#else
     const int full = !pp || (progress_peer(a.sys, pp + min(r + 3, a.hmb - 1)) >= want &&
                              progress_peer(a.sys, pp + min(r + 2, a.hmb - 1)) >= want);
+#endif
     if (full && pp) {  // acquire what the progress words released (the loads below follow the barrier)
       acquire_fence(a.sys);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
