@@ -1639,6 +1639,13 @@ struct alignas(16) RowLds {
 #endif
 };
 
+// The row coder's first load of the row above's fresh granules before its
+// group-start wait (1) or after it (0).
+#ifndef CAIRO_EARLY_GRAN
+#define CAIRO_EARLY_GRAN 1
+#endif
+constexpr bool kEarlyGran = CAIRO_EARLY_GRAN;
+
 // Deblock chunks the coder may leave pending at a group start before it runs
 // a ready one even when its inter records are already there (the next
 // frame's helpers wait for this row's progress).
@@ -1936,6 +1943,13 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       trace(tr, 2, (int)a.epoch * 1000 + by);
       stamp(a, mb, 0);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
+      // The row above's fresh column block (bx+2, by-1): its first granule
+      // load is issued before the group-start wait below, so that a granule
+      // already there costs no round trip after it (the tag is the flag: a
+      // 64-bit load needs no acquire).
+      const bool fresh_col = by > 0 && bx != 0 && bx + 2 < a.wmb && tid < kGranulesPerMB;
+      const uint64_t* fresh_gp = fresh_col ? gran_at(a, bx + 2, by - 1, tid) : nullptr;
+      const uint64_t fresh_g = (kEarlyGran && fresh_col) ? gran_ld(fresh_gp) : 0;
       if ((bx & 3) == 0) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
 #if CAIRO_CODER_DEBLOCK
         coder_wait(a, by, bx, L.db, dst, flag);
@@ -1962,9 +1976,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
             const uint64_t* gp = gran_at(a, lx[i], ly[i], kk);
             win_put_k(L.win, oy, lx[i], ly[i], kk, gran_settle(gp, gran_ld(gp), tag, err, a.sticky));
           }
-        } else if (bx + 2 < a.wmb && tid < kGranulesPerMB) {
-          const uint64_t* gp = gran_at(a, bx + 2, by - 1, tid);
-          win_put_k(L.win, oy, bx + 2, by - 1, tid, gran_settle(gp, gran_ld(gp), tag, err, a.sticky));
+        } else if (fresh_col) {
+          win_put_k(L.win, oy, bx + 2, by - 1, tid,
+                    gran_settle(fresh_gp, kEarlyGran ? fresh_g : gran_ld(fresh_gp), tag, err, a.sticky));
         }
       }
       // source rows of this lane's group slot
