@@ -23,11 +23,12 @@ Other legs (rank 0, N = 1), outside the timed region:
               host RGB in, bitstream out: the reference's own interface)
   cpu_baseline  the oracle (C restatement) on one host core, bounded sample
 
-Multi-GPU: one process per GPU (torch.distributed.run).  value: every rank
-encodes its own stream (replicas, weak scaling), the aggregate.  single_stream
-(N > 1): ONE stream over all ranks, frame-interleaved (rank k encodes frames
-n = k mod N, reading the others' reconstructions in place over xGMI; strong
-scaling over the same frames as N = 1), DESIGN.md §6.
+Multi-GPU: one process per GPU (torch.distributed.run).  value (N > 1): ONE
+stream over all ranks (BASELINE.json configs[3]: one 4K stream over the
+node), frame-interleaved (rank k encodes frames n = k mod N, reading the
+others' reconstructions, mirrored into its own memory over xGMI; strong
+scaling over the same frames as N = 1); replicas (every rank
+encodes its own stream, weak scaling) ride along as an extra field.
 """
 from __future__ import annotations
 
@@ -119,6 +120,34 @@ def max_over_ranks(x: float, dist, device) -> float:
 def aggregate_mpix(w: int, h: int, frames: int, world: int, elapsed_max: float) -> float:
     """Whole-job throughput: every rank encodes `frames` frames of w x h (weak scaling)."""
     return w * h * frames * world / elapsed_max / 1e6
+
+
+def headline(world: int, replicas: dict, single: dict | None) -> dict:
+    """The line's value at N GPUs: N = 1, the one context's stream; N > 1,
+    the one stream over all ranks (single_stream, strong scaling: the metric
+    of BASELINE.json configs[3]), unless that leg failed or was skipped --
+    then the replicas' aggregate, labelled as such (weak scaling).
+    replicas = {"value", "ms_per_step"}; -> {"value", "scaling", "value_source",
+    "ms_per_step"}."""
+    if world == 1:
+        return {"value": replicas["value"], "scaling": "weak", "value_source": "one stream on one GPU",
+                "ms_per_step": replicas["ms_per_step"]}
+    if single and single.get("value") is not None and not single.get("error"):
+        return {"value": single["value"], "scaling": "strong",
+                "value_source": f"single_stream: one stream over {world} GPUs (frame-interleaved group)",
+                "ms_per_step": single["ms_per_step"]}
+    why = (single or {}).get("error") or "single-stream leg skipped"
+    return {"value": replicas["value"], "scaling": "weak",
+            "value_source": f"replicas: {world} independent streams (single_stream unavailable: {why})"[:400],
+            "ms_per_step": replicas["ms_per_step"]}
+
+
+def single_stream_check_frames(world: int, ring: int, warm: int) -> int:
+    """Frames of the single-stream leg compared with the oracle: at least 2N
+    + R, so that every member's frames (each member twice) and every mirror
+    push (a frame's reconstruction is pushed to the members of its next R
+    frames) are compared; at least 8; at most the warm-up frames."""
+    return min(max(2 * world + ring, 8), warm)
 
 
 def cpu_model() -> str:
@@ -305,6 +334,10 @@ def main():
     elapsed = max_over_ranks(elapsed, dist, dev)
     value = aggregate_mpix(w, h, timed_frames, world, elapsed)
     note(rank, f"timed region: {timed_frames} frames in {elapsed:.3f} s")
+    replicas = {"value": round(value, 3), "unit": "Mpix/s", "scaling": "weak", "streams": world,
+                "ms_per_step": round(elapsed * 1e3 / a.steps, 4), "ms_per_frame": round(elapsed * 1e3 / timed_frames, 4),
+                "timed_frames_per_rank": timed_frames,
+                "note": "every rank encodes its own stream (independent replicas); whole-job aggregate"}
     kf = max(kframes, 1)
     abytes = algorithmic_bytes(w, h, ring)
     engine_busy_ms = kernel_ms[3] / kf  # union of the launch intervals / frames
@@ -376,25 +409,31 @@ def main():
         note(rank, "encode() API leg")
         api = api_encode(w, h, ring, q, 2 + max(4, min(12, int(100e6 / (w * h)))))
 
+    head = headline(world, replicas, single)
+    where = "on one GPU" if world == 1 else f"as one stream over {world} GPUs"
     result = {
         "metric": "encoded Mpixels/s (p-frame, q=16) at 1/2/4/8 MI355X; bit-exact vs ref",
-        "value": round(value, 3),
+        "value": head["value"],
         "unit": "Mpix/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": round(value / REF_CPU_MPIX[a.config], 1) if a.config in REF_CPU_MPIX else None,
-        "vs_baseline_note": "value / BASELINE.md's reference CPU encode (one Xeon core, measured in the survey; "
-                            "the reference publishes no number)",
+        "scaling": head["scaling"],
+        "value_source": head["value_source"],
+        # the reference publishes no number (its CPU figures are
+        # the survey's own measurements), so no vs_baseline; the CPU ratios
+        # below name their denominators
+        "vs_baseline": None,
         "dtype": "int16",
         "data": "synthetic (band4 generator, seed 1234; SURVEY.md §8(d)), resident in HBM",
-        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}] on one GPU)",
+        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}] {where})",
                    "width": w, "height": h, "ring": ring, "quality": q, "frames_per_step": batch,
-                   "timed_frames": timed_frames, "ms_per_frame": round(elapsed * 1e3 / timed_frames, 4),
-                   "parallelism": f"replicas: {world} independent stream(s), one per GPU"},
+                   "timed_frames": timed_frames, "ms_per_frame": round(head["ms_per_step"] / batch, 4),
+                   "parallelism": "one stream on one GPU" if world == 1 else
+                   f"single stream, frame-interleaved over {world} GPUs (member k encodes frames n = k mod {world})"},
+        "replicas": replicas if world > 1 else None,
         "roofline": roof,
         "roofline_valu": valu,
         "end_to_end": e2e,
@@ -408,6 +447,15 @@ def main():
                                                                    hot_records, e2e_records, batch)
     else:
         result["cpu_baseline"] = None
+    vs = {}
+    if a.config in REF_CPU_MPIX:
+        vs["survey_xeon_reference"] = round(result["value"] / REF_CPU_MPIX[a.config], 1)
+    if result["cpu_baseline"]:
+        vs["this_box_oracle"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+    result["vs_cpu"] = dict(vs, note="value / a one-core CPU encode: survey_xeon_reference = the reference itself "
+                                     "on one Xeon core of the survey container (BASELINE.md, not a published "
+                                     "number); this_box_oracle = cpu_baseline.value (the oracle, a C restatement "
+                                     "of the reference, on one core of this box)")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
@@ -448,7 +496,7 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
 
     gloo = dist.new_group(backend="gloo")
     res, err = None, ""
-    n_check = 4
+    n_check = single_stream_check_frames(world, ring, warm)
     recs = {}
     ctx = None
     state = {"err": ""}
@@ -504,6 +552,9 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
         res = time.perf_counter() - t0
         note(rank, "single stream: timed run done")
     err = state["err"]
+    mine = len(range(rank, timed, world))  # this member's frames of the timed region
+    per_member = [None] * world
+    dist.all_gather_object(per_member, round(res * 1e3 / max(mine, 1), 4) if res else None, group=gloo)
     ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=gloo)
     elt = torch.tensor([res or 0.0], dtype=torch.float64)
@@ -519,9 +570,12 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
         return {"error": [e for e in errs if e]}
     el = float(elt.item())
     out = {"value": round(aggregate_mpix(w, h, timed, 1, el), 3), "unit": "Mpix/s", "scaling": "strong",
-           "members": world, "ms_per_frame": round(el * 1e3 / timed, 4), "timed_frames": timed,
-           "note": "one stream, frame n on rank n % N (frame-interleaved group, in-place reads over xGMI); same "
-                   "frames as the N = 1 run"}
+           "members": world, "world_size_seen": dist.get_world_size(),
+           "backend": dist.get_backend(), "ms_per_frame": round(el * 1e3 / timed, 4),
+           "ms_per_step": round(el * 1e3 / max(1, timed // batch), 4), "timed_frames": timed,
+           "member_ms_per_own_frame": per_member,
+           "note": "one stream, frame n on rank n % N (frame-interleaved group; each frame's reconstruction "
+                   "pushed into the memory of the members that read it); same frames as the N = 1 run"}
     if rank == 0:
         from oracle import oracle as orc
 
@@ -536,7 +590,8 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
             if t not in got or orc.canonical_frame_bytes(got[t][0], got[t][1], t == 0) != \
                     orc.canonical_frame_bytes(data, nb, t == 0):
                 mism.append(t)
-        out["bit_exact"] = {"frames_checked": n_check, "mismatched_frames": mism, "bit_exact": not mism}
+        out["bit_exact"] = {"frames_checked": n_check, "members_covered": min(world, n_check),
+                            "mismatched_frames": mism, "bit_exact": not mism}
     return out
 
 

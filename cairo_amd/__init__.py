@@ -47,10 +47,20 @@ MAX_BATCH = 32  # kMaxBatch (kernels.h): frames per engine launch, stamp layout
 EVX_ERROR_HARDWAREFAIL = 5
 
 
+# In-kernel wait kinds of a timeout record (include/cairo_amd.h CAIRO_WAIT_*)
+WAIT_KINDS = {1: "records", 2: "granule", 3: "prev_progress", 4: "row_above", 5: "batch", 6: "injected",
+              9: "host_mark"}
+TIMEOUT_FIELDS = ("kind", "epoch", "index", "row", "member", "need", "on", "seen_lo", "seen_hi")
+
+
 class CairoError(RuntimeError):
-    def __init__(self, what: str, status: int):
-        super().__init__(f"{what} failed with evx_status {status}")
+    def __init__(self, what: str, status: int, timeout: dict | None = None):
+        msg = f"{what} failed with evx_status {status}"
+        if timeout:
+            msg += f" (in-kernel wait timed out: {timeout})"
+        super().__init__(msg)
         self.status = status
+        self.timeout = timeout  # the first timed-out wait (Context.timeout_info), if one was reported
 
 
 _lib = None
@@ -90,14 +100,15 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_set_batch": (I, [P, I]),
         "cairo_ctx_peer_info": (I, [P, I, P]),
         "cairo_ctx_join_group": (I, [P, I, I, P]),
-        "cairo_group_check_queues": (I, [I]),
+        "cairo_group_check_queues": (I, [I, I]),
+        "cairo_ctx_timeout_info": (I, [P, P, I]),
         "cairo_peer_size": (I, []),
         "cairo_ctx_flush": (I, [P]),
         "cairo_ctx_set_helpers": (I, [P, I]),
         "cairo_ctx_max_workgroups": (I, [P]),
         "cairo_default_batch": (I, [U, U]),
         "cairo_task_order": (I, [I, I, P, ctypes.POINTER(I)]),
-        "cairo_task_queues": (I, [I, I, P, P, ctypes.POINTER(I)]),
+        "cairo_task_queues": (I, [I, I, I, I, I, P, P, ctypes.POINTER(I)]),
         "cairo_kat_transform": (I, [P, P, P, I, P, P, P, I]),
         "cairo_serialize_slice": (I, [P, U, U, U, P, P, P, P, U, ctypes.POINTER(U)]),
         "cairo_serialize_feed": (I, [P, ctypes.c_uint64, P, U, ctypes.POINTER(U)]),
@@ -252,9 +263,25 @@ class Context:
 
     def wait(self, ticket: int, copy: bool = True) -> FrameOutputs:
         r = _FrameResult()
-        _ck(self.L.cairo_ctx_wait(self.h, ticket, ctypes.byref(r)), "cairo_ctx_wait")
+        st = self.L.cairo_ctx_wait(self.h, ticket, ctypes.byref(r))
+        if st != EVX_SUCCESS:
+            raise CairoError("cairo_ctx_wait", st, self.timeout_info() if st == EVX_ERROR_HARDWAREFAIL else None)
         self._keep.pop(ticket, None)
         return self._outputs(r, copy)
+
+    def timeout_info(self) -> dict | None:
+        """The in-kernel wait that timed out first, as last reported
+        (cairo_ctx_timeout_info): kind (WAIT_KINDS name), the waiting frame's
+        epoch, index and MB row, the group member, what it needed, what it
+        waited on, the last value seen; None if none since create / reset."""
+        w = np.zeros(16, np.int32)
+        _ck(self.L.cairo_ctx_timeout_info(self.h, _ptr(w), 16), "cairo_ctx_timeout_info")
+        if not w[0]:
+            return None
+        d = {k: int(w[i]) for i, k in enumerate(TIMEOUT_FIELDS)}
+        d["kind"] = WAIT_KINDS.get(d["kind"], str(d["kind"]))
+        d["seen"] = (d.pop("seen_hi") & 0xFFFFFFFF) << 32 | (d.pop("seen_lo") & 0xFFFFFFFF)
+        return d
 
     def _outputs(self, r, copy: bool) -> FrameOutputs:
         ny, nc = r.wa * r.ha, (r.wa // 2) * (r.ha // 2)
@@ -498,13 +525,16 @@ def task_order(hmb: int, frames: int):
     return out, slope.value
 
 
-def task_queues(hmb: int, frames: int):
-    """-> (the launch's tasks partitioned into per-label queues: int32 (frame
-    << 16 | row), the 9 segment bounds, the number of labels)."""
+def task_queues(hmb: int, frames: int, helpers: int = 192, rows: int = 192, pool: int = 0):
+    """-> (one pool's tasks (0 helpers, 1 row coders) of a launch with
+    `helpers` + `rows` workers, partitioned into per-label queues: int32
+    (frame << 16 | row), the 9 segment bounds, the number of labels) -- the
+    layout the engine's launch uses (backend.hip banded_pool)."""
     out = np.zeros(frames * hmb, np.int32)
     seg = np.zeros(9, np.int32)
     nlab = ctypes.c_int()
-    _ck(lib().cairo_task_queues(hmb, frames, _ptr(out), _ptr(seg), ctypes.byref(nlab)), "cairo_task_queues")
+    _ck(lib().cairo_task_queues(hmb, frames, helpers, rows, pool, _ptr(out), _ptr(seg), ctypes.byref(nlab)),
+        "cairo_task_queues")
     return out, seg, nlab.value
 
 

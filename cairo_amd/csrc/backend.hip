@@ -68,10 +68,16 @@ constexpr int kSuccess = 0, kInvalidArg = 1, kOutOfMemory = 3, kHardwareFail = 5
               kInvalidResource = 8;
 
 struct Stage {
-  uint8_t* table = nullptr;  // pinned
+  uint8_t* table = nullptr;  // pinned, mapped (k_feed_copy writes it in feed mode)
   int16_t* coef = nullptr;   // pinned, 1.5 * wa * ha
-  int32_t* err = nullptr;    // pinned, 1 word
+  int32_t* err = nullptr;    // pinned, mapped: the context's TimeoutInfo words after the frame
+  uint8_t* table_dev = nullptr;  // device addresses of table / err
+  int32_t* err_dev = nullptr;
   hipEvent_t d2h_done = nullptr;
+  // The launch that converts this slot's staged host RGB: a later frame's
+  // upload into the same staging buffer waits for it (rgb_read).
+  hipEvent_t rgb_read = nullptr;
+  bool rgb_pending = false;
   int ticket = -1;
   bool busy = false;      // submitted, not yet released
   bool launched = false;  // its batch has been launched
@@ -173,7 +179,9 @@ struct cairo_ctx {
   hipEvent_t pre_done[kSyncAreas] = {};
   bool ps_own = getenv("CAIRO_PRECODE_OWN_STREAM") != nullptr;  // A/B switch
   bool sys = false;           // a member is another process or device: system-scope hand-offs
-  int32_t *sync = nullptr, *sticky = nullptr;
+  int32_t *sync = nullptr;
+  int32_t* sticky = nullptr;  // TimeoutInfo words (kernels.h), cleared only by zero_state
+  int inject = 0;             // test hook (cairo_ctx_set_debug 16): EngineArgs::inject
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
   FrameArgs* fdesc_host = nullptr;  // pinned [kLaunchSlots][kMaxBatch]: per-frame views per launch
   FrameArgs* fdesc = nullptr;       // device copy
@@ -212,6 +220,8 @@ struct cairo_ctx {
   // signalled when a batch launches.
   std::mutex mu;
   std::condition_variable launched_cv;
+  std::mutex tmu;                             // guards timeout (written by threads waiting outside mu)
+  int32_t timeout[TimeoutInfo::kWords] = {};  // the last reported TimeoutInfo words
 };
 
 namespace {
@@ -241,13 +251,23 @@ PlaneSet coef_planes(const cairo_ctx* c, int slot) { return planes_at(coef_base(
 PlaneSet peer_coef_planes(const cairo_ctx::Peer& p, const cairo_ctx* c, int slot) {
   return planes_at(p.coef[slot / p.coef_per] + (size_t)(slot % p.coef_per) * c->plane_elems, c);
 }
-// Allocate the output_cache chunks (fine-grained for cross-device sharing);
-// on failure nothing stays allocated.
+// Allocate the output_cache: one allocation for a context nobody imports;
+// fine-grained chunks of at most kCoefChunkBytes, each exported with its own
+// IPC handle, for cross-device sharing (cairo_ctx_peer_info).  On failure
+// nothing stays allocated.
 hipError_t alloc_coef(const cairo_ctx* c, bool fine, int16_t* out[CAIRO_MAX_COEF_CHUNKS], int* chunks, int* per) {
   const size_t slot_bytes = c->plane_elems * 2;
-  const int p = (int)std::max<size_t>(1, std::min<size_t>((size_t)c->stages, kCoefChunkBytes / slot_bytes));
+  if (fine && slot_bytes > kCoefChunkBytes) {
+    fprintf(stderr, "[cairo_amd] peer_info: one output_cache slot (%zu bytes) exceeds the %zu-byte IPC export limit\n",
+            slot_bytes, kCoefChunkBytes);
+    return hipErrorInvalidValue;
+  }
+  const int p = fine ? (int)std::min<size_t>((size_t)c->stages, kCoefChunkBytes / slot_bytes) : c->stages;
   const int n = (c->stages + p - 1) / p;
-  if (n > CAIRO_MAX_COEF_CHUNKS) return hipErrorInvalidValue;
+  if (n > CAIRO_MAX_COEF_CHUNKS) {
+    fprintf(stderr, "[cairo_amd] peer_info: %d output_cache chunks needed, at most %d\n", n, CAIRO_MAX_COEF_CHUNKS);
+    return hipErrorInvalidValue;
+  }
   for (int k = 0; k < CAIRO_MAX_COEF_CHUNKS; k++) out[k] = nullptr;
   for (int k = 0; k < n; k++) {
     const size_t bytes = slot_bytes * (size_t)std::min(p, c->stages - k * p);
@@ -284,6 +304,7 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.gran_base = c->gran;
   e.sync = c->sync;
   e.sticky = c->sticky;
+  e.inject = c->inject;
   e.stamps = c->stamps;
   e.trace = c->trace_dev;
   return e;
@@ -360,6 +381,14 @@ std::vector<int32_t> order_block(int hmb, int slope) {
   return blk;
 }
 
+// Whether a launch's pool uses per-label (XCD-banded) queues: frames of at
+// least kBandMinRows macroblock rows, both pools splitting evenly over the
+// labels, and the pool enabled in kBandPools.  flush() and cairo_task_queues
+// share it, so the tests check the layout the engine runs.
+bool banded_pool(int hmb, int n_helpers, int n_rows, int pool) {
+  return hmb >= kBandMinRows && n_helpers % kLabels == 0 && n_rows % kLabels == 0 && ((kBandPools >> pool) & 1);
+}
+
 int upload_orders(cairo_ctx* c, int slope) {
   c->order_slope = slope;
   const std::vector<int32_t> blk = order_block((int)c->hmb, slope);
@@ -380,6 +409,7 @@ void free_ctx(cairo_ctx* c) {
     if (s.coef) (void)hipHostFree(s.coef);
     if (s.err) (void)hipHostFree(s.err);
     if (s.d2h_done) (void)hipEventDestroy(s.d2h_done);
+    if (s.rgb_read) (void)hipEventDestroy(s.rgb_read);
   }
   for (auto& t : c->tb)
     for (auto& e : t.ev)
@@ -434,8 +464,12 @@ int zero_state(cairo_ctx* c) {
   CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * S, c->ks));
   CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t) * kSyncAreas, c->ks));
   CK(hipMemsetAsync(c->progress, 0, (size_t)c->hmb * sizeof(uint64_t) * S, c->ks));
-  CK(hipMemsetAsync(c->sticky, 0, sizeof(int32_t), c->ks));
+  CK(hipMemsetAsync(c->sticky, 0, TimeoutInfo::kWords * sizeof(int32_t), c->ks));
   CK(hipStreamSynchronize(c->ks));
+  {
+    std::lock_guard<std::mutex> lk(c->tmu);
+    memset(c->timeout, 0, sizeof(c->timeout));
+  }
   c->epoch = 0;
   c->last_slot = -1;
   c->batches = 0;
@@ -447,7 +481,7 @@ int zero_state(cairo_ctx* c) {
   // locate its output_cache and progress words (frame_links)
   c->next_ticket = 0;
   for (auto& s : c->st) {
-    *s.err = 0;
+    memset(s.err, 0, TimeoutInfo::kWords * sizeof(int32_t));
     s.ticket = -1;
   }
   return kSuccess;
@@ -519,9 +553,8 @@ int flush(cairo_ctx* c) {
   }
   // XCD-banded queues (kernels.h kLabels) on large frames, when both pools
   // split evenly over the labels
-  const int banded = c->hmb >= (uint32_t)kBandMinRows && e.n_helpers % kLabels == 0 && e.n_rows % kLabels == 0;
   for (int k = 0; k < 2; k++) {
-    const int bk = banded && (kBandPools >> k & 1);
+    const int bk = banded_pool((int)c->hmb, e.n_helpers, e.n_rows, k);
     e.nlab[k] = bk ? kLabels : 1;
     e.order[k] = c->order + OrderBlock::order_at((int)c->hmb, bk, e.nframes);
     e.seg[k] = c->order + OrderBlock::seg_at((int)c->hmb, bk, e.nframes);
@@ -561,6 +594,14 @@ int flush(cairo_ctx* c) {
   }
   if (tb) CK(hipEventRecord(tb->ev[0], st));
   CK(launch_convert_batch(e, st));
+  for (int i = 0; i < e.nframes; i++) {  // staged host RGB converted: the buffer may be refilled
+    const FrameDesc& f = c->pend[i];
+    Stage& s = c->st[f.slot];
+    if (!f.decode && f.rgb == c->rgb + (size_t)f.slot * c->w * c->h * 3) {
+      CK(hipEventRecord(s.rgb_read, st));
+      s.rgb_pending = true;
+    }
+  }
   CK(hipEventRecord(c->batch_ready[area], st));
   // the previous batch's tasks, which this launch's workers may run, need its
   // frames converted and its views and sync area in place
@@ -601,6 +642,15 @@ int flush(cairo_ctx* c) {
     fa.feed = c->feed_dev;
     fa.feed_stride = c->feed_words;
     fa.hdr = c->feed_hdr;
+    // each frame's block table and the timeout words go to its mapped pinned
+    // stage in the same kernel as the feed: no D2H copy per frame, whose
+    // shader blit waits for a workgroup slot of the persistent engine
+    for (int i = 0; i < e.nframes; i++) {
+      const Stage& s = c->st[fa.slot[i]];
+      fa.table_host[i] = c->pend[i].decode ? nullptr : (uint4*)s.table_dev;
+      fa.err_host[i] = c->pend[i].decode ? nullptr : s.err_dev;
+    }
+    fa.table_words = (int)(c->mbs * sizeof(BlockDesc) / sizeof(uint4));
     CK(launch_precode(fa, (int)c->mbs, pst));
   }
   if (!c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
@@ -610,7 +660,10 @@ int flush(cairo_ctx* c) {
   } else {
     CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
   }
-  // outputs for the host entropy stage, on the copy stream
+  // outputs for the host entropy stage: with the feed, the precode's last
+  // kernel (k_feed_copy) has written each frame's feed, block table and
+  // timeout words into its mapped pinned stage; the coefficient planes (and,
+  // without the feed, the table and timeout words) go D2H on the copy stream
   for (int i = 0; i < e.nframes; i++) {
     const int slot = c->pend[i].slot;
     Stage& s = c->st[slot];
@@ -618,12 +671,17 @@ int flush(cairo_ctx* c) {
       s.launched = true;
       continue;
     }
-    CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
-                      hipMemcpyDeviceToHost, c->cs));
-    if (c->outputs & CAIRO_OUT_COEF)
+    if (c->outputs & CAIRO_OUT_COEF) {
+      if (!(c->outputs & CAIRO_OUT_FEED)) {
+        CK(hipMemcpyAsync(s.table, c->table + (size_t)slot * c->mbs, c->mbs * sizeof(BlockDesc),
+                          hipMemcpyDeviceToHost, c->cs));
+        CK(hipMemcpyAsync(s.err, c->sticky, TimeoutInfo::kWords * sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
+      }
       CK(hipMemcpyAsync(s.coef, coef_base(c, slot), c->plane_elems * 2, hipMemcpyDeviceToHost, c->cs));
-    CK(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, c->cs));
-    CK(hipEventRecord(s.d2h_done, c->cs));
+      CK(hipEventRecord(s.d2h_done, c->cs));
+    } else {
+      CK(hipEventRecord(s.d2h_done, pst));
+    }
     s.launched = true;
   }
   c->last_slot = last;
@@ -786,8 +844,8 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * S));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t) * kSyncAreas));
   TRY(hipMalloc(&c->progress, (size_t)c->hmb * sizeof(uint64_t) * S));
-  TRY(hipMalloc(&c->sticky, sizeof(int32_t)));
-  TRY(hipMemset(c->sticky, 0, sizeof(int32_t)));
+  TRY(hipMalloc(&c->sticky, TimeoutInfo::kWords * sizeof(int32_t)));
+  TRY(hipMemset(c->sticky, 0, TimeoutInfo::kWords * sizeof(int32_t)));
   {  // (frame, row) task order of the engine pools, for every batch size
     TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch, hipHostMallocDefault));
     TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch));
@@ -799,10 +857,14 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
     }
   }
   for (auto& s : c->st) {
-    TRY(hipHostMalloc(&s.table, c->mbs * sizeof(BlockDesc), hipHostMallocDefault));
+    TRY(hipHostMalloc(&s.table, c->mbs * sizeof(BlockDesc), hipHostMallocMapped));
     TRY(hipHostMalloc(&s.coef, c->plane_elems * 2, hipHostMallocDefault));
-    TRY(hipHostMalloc(&s.err, sizeof(int32_t), hipHostMallocDefault));
+    TRY(hipHostMalloc(&s.err, TimeoutInfo::kWords * sizeof(int32_t), hipHostMallocMapped));
+    memset(s.err, 0, TimeoutInfo::kWords * sizeof(int32_t));
+    TRY(hipHostGetDevicePointer((void**)&s.table_dev, s.table, 0));
+    TRY(hipHostGetDevicePointer((void**)&s.err_dev, s.err, 0));
     TRY(hipEventCreateWithFlags(&s.d2h_done, hipEventDisableTiming));
+    TRY(hipEventCreateWithFlags(&s.rgb_read, hipEventDisableTiming));
   }
   for (auto& t : c->tb)
     for (auto& e : t.ev) TRY(hipEventCreate(&e));
@@ -857,10 +919,13 @@ int cairo_task_order(int hmb, int frames, int32_t* out, int* slope) {
   return kSuccess;
 }
 
-int cairo_task_queues(int hmb, int frames, int32_t* order, int32_t* seg, int* nlab) {
-  if (hmb < 1 || hmb > 0xFFFF || frames < 1 || frames > kMaxBatch || !order || !seg) return kInvalidArg;
+int cairo_task_queues(int hmb, int frames, int n_helpers, int n_rows, int pool, int32_t* order, int32_t* seg,
+                      int* nlab) {
+  if (hmb < 1 || hmb > 0xFFFF || frames < 1 || frames > kMaxBatch || !order || !seg || n_helpers < 1 || n_rows < 1 ||
+      pool < 0 || pool > 1)
+    return kInvalidArg;
   const std::vector<int32_t> blk = order_block(hmb, kOrderSlope);
-  const int banded = hmb >= kBandMinRows;
+  const int banded = banded_pool(hmb, n_helpers, n_rows, pool);
   memcpy(order, &blk[OrderBlock::order_at(hmb, banded, frames)], (size_t)frames * hmb * sizeof(int32_t));
   memcpy(seg, &blk[OrderBlock::seg_at(hmb, banded, frames)], (kLabels + 1) * sizeof(int32_t));
   if (nlab) *nlab = banded ? kLabels : 1;
@@ -932,10 +997,9 @@ int cairo_ctx_busy_intervals(cairo_ctx* c, double* out, int cap, int* n) {
   if (!c || !n || cap < 0 || (cap && !out)) return kInvalidArg;
   std::lock_guard<std::mutex> lk(c->mu);
   CK(hipSetDevice(c->device));
-  int r = flush(c);
-  if (r) return r;
+  // read-only: the launches made so far (a pending partial batch stays pending)
   for (auto& t : c->tb) {
-    r = collect_times(c, t);
+    const int r = collect_times(c, t);
     if (r) return r;
   }
   std::vector<std::pair<double, double>> iv = c->busy;
@@ -976,13 +1040,27 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   } else {  // the caller keeps it valid until wait
     f.rgb = c->rgb + (size_t)slot * c->w * c->h * 3;
     f.host_rgb = rgb;
-    if (c->gsize == 1) {  // uploaded now, beside the launches in flight (the slot's last reader is done: released)
-      if (!c->us) {
-        CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
-        CK(hipEventCreateWithFlags(&c->up_last, hipEventDisableTiming));
+    if (c->gsize == 1) {
+      // Uploaded now, beside the launches in flight.  The staging buffer's
+      // previous frame may still wait for its conversion (a caller may release
+      // a ticket without waiting for it): the upload waits for the launch that
+      // converts it (rgb_read).  With feed outputs only, the copy stream has
+      // no other work (the outputs come from k_feed_copy), so the uploads use
+      // it; with coefficient D2H copies queued there they get a stream of
+      // their own (GPU_MAX_HW_QUEUES is 4 by default: a fifth stream shares a
+      // hardware queue with one of these).
+      hipStream_t up = c->cs;
+      if (c->outputs & CAIRO_OUT_COEF) {
+        if (!c->us) CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
+        up = c->us;
       }
-      CK(hipMemcpyAsync((void*)f.rgb, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, c->us));
-      CK(hipEventRecord(c->up_last, c->us));
+      if (!c->up_last) CK(hipEventCreateWithFlags(&c->up_last, hipEventDisableTiming));
+      if (s.rgb_pending) {
+        CK(hipStreamWaitEvent(up, s.rgb_read, 0));
+        s.rgb_pending = false;
+      }
+      CK(hipMemcpyAsync((void*)f.rgb, rgb, (size_t)c->w * c->h * 3, hipMemcpyHostToDevice, up));
+      CK(hipEventRecord(c->up_last, up));
       c->up_pending = true;
       f.host_rgb = nullptr;
     }
@@ -998,6 +1076,7 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   // them by stream index)
   f.epoch = c->gsize > 1 ? index + 1 : ++c->epoch;
   f.slot = slot;
+  f.member = c->grank;
   f.decode = 0;  // decode_frame never leaves a decode frame pending
   f.host_table = nullptr;
   f.host_coef = nullptr;
@@ -1013,6 +1092,34 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
   *ticket = t;
   if (c->npend >= c->batch_max) return flush(c);
   return kSuccess;
+}
+
+static const char* timeout_kind_name(int k) {
+  switch (k) {
+    case kWaitRecords: return "inter records (row coder)";
+    case kWaitGranule: return "granule";
+    case kWaitPrevProgress: return "previous frame's deblock progress (row helper)";
+    case kWaitRowAbove: return "row above's deblock progress (deblock)";
+    case kWaitBatch: return "batch completion";
+    case kWaitInjected: return "injected (test hook)";
+    case kWaitHostMark: return "marked by the host (test hook)";
+    default: return "unknown";
+  }
+}
+
+// A frame found the context's timeout words set: say on stderr which wait
+// gave up first, and keep the words for cairo_ctx_timeout_info.
+static void report_timeout_host(cairo_ctx* c, const int32_t* w, uint32_t index) {
+  {
+    std::lock_guard<std::mutex> lk(c->tmu);
+    memcpy(c->timeout, w, sizeof(c->timeout));
+  }
+  using T = TimeoutInfo;
+  fprintf(stderr,
+          "[cairo_amd] an in-kernel wait timed out (reported at frame %u): %s; member %d, frame index %d (epoch %u), "
+          "MB row %d, waiting on %d (0x%x) for %d, last seen 0x%08x%08x\n",
+          index, timeout_kind_name(w[T::kKind]), w[T::kMember], w[T::kIndex], (uint32_t)w[T::kEpoch], w[T::kRow],
+          w[T::kOn], (uint32_t)w[T::kOn], w[T::kNeed], (uint32_t)w[T::kSeenHi], (uint32_t)w[T::kSeenLo]);
 }
 
 // Frame outputs once its D2H finished (called without mu held).  poll: wait
@@ -1032,8 +1139,8 @@ static int frame_result(cairo_ctx* c, Stage& s, cairo_frame_result* out, bool po
   } else {
     CK(hipEventSynchronize(s.d2h_done));
   }
-  if (*s.err) {
-    fprintf(stderr, "[cairo_amd] an in-kernel wait timed out (at or before frame %u)\n", s.index);
+  if (s.err[TimeoutInfo::kKind]) {
+    report_timeout_host(c, s.err, s.index);
     return kHardwareFail;
   }
   out->block_table = s.table;
@@ -1120,12 +1227,13 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
     r = fail(launch_yuv_to_rgb(slot_planes(c->ring_buf, c, (int)(index % c->ring)), (int)c->wa, (int)c->w,
                                (int)c->h, drgb, st), "launch_yuv_to_rgb");
     if (r == kSuccess)
-      r = fail(hipMemcpyAsync(s.err, c->sticky, sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+      r = fail(hipMemcpyAsync(s.err, c->sticky, TimeoutInfo::kWords * sizeof(int32_t), hipMemcpyDeviceToHost, st),
+               "hipMemcpyAsync");
     if (r == kSuccess)
       r = fail(hipMemcpyAsync(rgb, drgb, (size_t)c->w * c->h * 3, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     if (r == kSuccess) r = fail(hipStreamSynchronize(st), "hipStreamSynchronize");
-    if (r == kSuccess && *s.err) {
-      fprintf(stderr, "[cairo_amd] an in-kernel wait timed out (decoding frame %u)\n", index);
+    if (r == kSuccess && s.err[TimeoutInfo::kKind]) {
+      report_timeout_host(c, s.err, index);
       r = kHardwareFail;
     }
   }
@@ -1134,6 +1242,13 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
 }
 
 int cairo_ctx_max_workgroups(const cairo_ctx* c) { return c ? c->max_rows : 0; }
+
+int cairo_ctx_timeout_info(cairo_ctx* c, int32_t* out, int n) {
+  if (!c || !out || n < 0 || n > TimeoutInfo::kWords) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->tmu);
+  memcpy(out, c->timeout, (size_t)n * sizeof(int32_t));
+  return kSuccess;
+}
 
 int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
   if (!c || outputs < 1 || outputs > (CAIRO_OUT_COEF | CAIRO_OUT_FEED)) return kInvalidArg;
@@ -1265,7 +1380,15 @@ int cairo_ctx_peer_info(cairo_ctx* c, int cross_device, cairo_peer* out) {
 
 int cairo_peer_size(void) { return (int)sizeof(cairo_peer); }
 
-int cairo_group_check_queues(int local_members) {
+// GPU_MAX_HW_QUEUES as the HIP runtime reads it: once, when it starts.  Read
+// here when the library is loaded (before any HIP call of ours); setting it
+// later in the process (os.environ after torch started HIP) changes nothing.
+static const int g_hw_queues = [] {
+  const char* env = getenv("GPU_MAX_HW_QUEUES");
+  return env && *env ? atoi(env) : 4;
+}();
+
+int cairo_group_check_queues(int local_members, int hw_queues) {
   // Members in one process on one device share that process's hardware
   // queues (GPU_MAX_HW_QUEUES, HIP's default 4).  Each member keeps two launch
   // streams and a copy stream busy; when two members' persistent launches
@@ -1273,8 +1396,7 @@ int cairo_group_check_queues(int local_members) {
   // ends, which waits on it: a deadlock the bounded in-kernel waits would
   // only report as EVX_ERROR_HARDWAREFAIL after 2 s.  Refuse up front.
   if (local_members < 2) return kSuccess;
-  const char* env = getenv("GPU_MAX_HW_QUEUES");
-  const int have = env && *env ? atoi(env) : 4;
+  const int have = hw_queues >= 0 ? hw_queues : g_hw_queues;
   const int need = 3 * local_members + 2;
   if (need > 32 || have < need) {
     fprintf(stderr,
@@ -1308,7 +1430,7 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
       }
     }
   }
-  if (cairo_group_check_queues(local) != kSuccess) return kInvalidArg;
+  if (cairo_group_check_queues(local, -1) != kSuccess) return kInvalidArg;
   for (int i = 0; i < size; i++) {
     cairo_ctx::Peer& q = c->gp[i];
     const cairo_peer& p = peers[i];
@@ -1429,9 +1551,10 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
     CK(hipHostGetDevicePointer((void**)&c->trace_dev, c->trace_host, 0));
   }
   if (flags & 8) {
-    const int32_t one = 1;
-    CK(hipMemcpy(c->sticky, &one, sizeof(one), hipMemcpyHostToDevice));
+    const int32_t mark = kWaitHostMark;
+    CK(hipMemcpy(c->sticky, &mark, sizeof(mark), hipMemcpyHostToDevice));
   }
+  c->inject = (flags & 16) ? 1 : 0;
   return kSuccess;
 }
 

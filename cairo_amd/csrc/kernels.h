@@ -48,6 +48,34 @@ __host__ __device__ inline size_t stamp_frame_words(int wmb, int hmb) {
   return (size_t)wmb * hmb * kStampPhases + (size_t)hmb * kDbStamps;
 }
 
+// Timeout diagnostics: the context's sticky words (int32, cleared only by a
+// reset).  Every in-kernel wait is bounded (2 s); the first one that gives up
+// records what it waited for, so a failed run (a cross-device group above all)
+// names the member, frame, row and word instead of only EVX_ERROR_HARDWAREFAIL.
+struct TimeoutInfo {
+  static constexpr int kKind = 0;    // TimeoutKind (0: no timeout)
+  static constexpr int kEpoch = 1;   // the waiting frame's epoch (granule tag)
+  static constexpr int kIndex = 2;   // its stream index
+  static constexpr int kRow = 3;     // the waiting task's MB row
+  static constexpr int kMember = 4;  // group rank of the waiting context (0 alone)
+  static constexpr int kNeed = 5;    // what it needed: columns, a count or a tag
+  static constexpr int kOn = 6;      // what it waited on: kind-specific (see TimeoutKind)
+  static constexpr int kSeenLo = 7;  // the last value it observed, low and high words
+  static constexpr int kSeenHi = 8;
+  static constexpr int kWords = 16;
+};
+enum TimeoutKind : int32_t {
+  kWaitRecords = 1,       // row coder: inter_done of group kOn < kNeed (= nref) records
+  kWaitGranule = 2,       // a granule of macroblock kOn (index in the frame) not tagged kNeed
+  kWaitPrevProgress = 3,  // row helper: frame epoch-back's progress word of row kOn & 0xFFFF
+                          // (back = kOn >> 16) below tagged(epoch - back, kNeed)
+  kWaitRowAbove = 4,      // deblock: row kRow-1's progress of this frame below kNeed columns
+  kWaitBatch = 5,         // k_batch_wait: kSeenLo of kNeed tasks finished
+  kWaitInjected = 6,      // test hook (cairo_ctx_set_debug 16): a helper's progress wait,
+                          // recorded as kWaitPrevProgress would be, without waiting
+  kWaitHostMark = 9,      // test hook (cairo_ctx_set_debug 8): marked by the host
+};
+
 // Frames per engine launch.
 #ifndef CAIRO_MAX_BATCH
 #define CAIRO_MAX_BATCH 32
@@ -82,6 +110,7 @@ struct FrameDesc {
   const uint64_t* prev_progress;  // the previous frame's (nullptr: none, first frame after a reset)
   const uint64_t* prev2_progress;  // frame index-2's (nullptr: none)
   int sys;                   // FrameArgs::sys
+  int member;                // FrameArgs::member
   const BlockDesc* host_table;  // decode: the frame's block table and coefficient planes (y, u, v
   const int16_t* host_coef;     //   contiguous), uploaded at launch
 };
@@ -120,7 +149,9 @@ struct FrameArgs {
   int32_t* inter_sad;     // [(off-1)*mbs + mb]
   uint64_t* granules;  // [mbs * kGranuleStride]
   int32_t* err;        // batch error word (a bounded wait timed out)
-  int32_t* sticky;     // timeout flag that is never cleared (reported by the host)
+  int32_t* sticky;     // TimeoutInfo words, never cleared by a launch (reported by the host)
+  int member;          // group rank of the encoding context (0 alone): timeout diagnostics
+  int inject;          // test hook: 1 = row helpers of row min(1, hmb-1) record an injected timeout
   int ng;              // inter-search groups (4 MBs) per row
   int nref;            // inter-search tasks per group (references; 1 carrier task for intra frames)
   int32_t* inter_done; // [hmb][ng] inter-search tasks finished
@@ -177,7 +208,8 @@ struct EngineArgs {
   int32_t* isad_base;      // stride nref * mbs
   uint64_t* gran_base;     // stride mbs * kGranuleStride
   int32_t* sync;           // SyncLayout words of this launch
-  int32_t* sticky;
+  int32_t* sticky;         // TimeoutInfo words
+  int inject;              // FrameArgs::inject
   uint64_t* stamps;
   int n_helpers, n_rows;   // worker pools (workgroups), spread over the block indices (is_helper)
   int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)

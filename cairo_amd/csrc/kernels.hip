@@ -209,19 +209,38 @@ __device__ __forceinline__ void acquire_fence(bool sys) {
 #define CAIRO_READY_PAIR 1
 #endif
 
-// Bounded wait on a progress word (relaxed agent-scope poll + s_sleep).  On
-// timeout (~2 s) the error word is set and the wait gives up, so every
-// workgroup still drains and the host reports EVX_ERROR_HARDWAREFAIL.
-__device__ __forceinline__ void wait_at_least(int32_t* word, int target, int32_t* err,
-                                              int32_t* sticky) {
-  if (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+// A bounded wait gave up (~2 s): set the launch's error word, so that every
+// other wait ends and every workgroup drains (the host then reports
+// EVX_ERROR_HARDWAREFAIL), and -- if no wait of this context gave up before --
+// record what this one waited for in the sticky words (kernels.h TimeoutInfo).
+// One lane; the cold path of every wait.
+__device__ __attribute__((noinline)) void report_timeout(int32_t* err, int32_t* sticky, int kind, uint32_t epoch,
+                                                         int index, int row, int member, int need, int on,
+                                                         uint64_t seen) {
+  __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int32_t none = 0;
+  if (!__hip_atomic_compare_exchange_strong(sticky + TimeoutInfo::kKind, &none, kind, __ATOMIC_RELAXED,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return;  // an earlier timeout is the one reported
+  const int32_t w[8] = {(int32_t)epoch, index, row, member, need, on, (int32_t)(uint32_t)seen, (int32_t)(seen >> 32)};
+  for (int k = 0; k < 8; k++) __hip_atomic_store(sticky + 1 + k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void report_timeout(FA& a, int kind, int row, int need, int on, uint64_t seen) {
+  report_timeout(a.err, a.sticky, kind, a.epoch, a.index, row, a.member, need, on, seen);
+}
+
+// Bounded wait of the row coder for its inter group's records (relaxed
+// agent-scope poll + s_sleep); gives up after ~2 s (report_timeout).
+__device__ __forceinline__ void wait_records(FA& a, int row, int group) {
+  int32_t* word = &a.inter_done[row * a.ng + group];
+  int v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (v >= a.nref) return;
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  while ((v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < a.nref) {
+    if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      report_timeout(a, kWaitRecords, row, a.nref, group, (uint32_t)v);
       return;
     }
   }
@@ -249,20 +268,19 @@ __device__ __forceinline__ uint64_t gran_ld(const uint64_t* p) {
 __device__ __forceinline__ void gran_st(uint64_t* p, uint64_t v) {
   __hip_atomic_store((gbl_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Data of granule p, given a first load g: re-polls until the tag matches.
-// Bounded like wait_at_least (the error word ends every other wait too).
-__device__ __forceinline__ uint32_t gran_settle(const uint64_t* p, uint64_t g, uint32_t tag,
-                                                int32_t* err, int32_t* sticky) {
-  if ((uint32_t)(g >> 32) == tag) return (uint32_t)g;
+// Data of granule p of frame a, given a first load g: re-polls until the tag
+// is the frame's epoch.  Bounded like every wait (the error word ends every
+// other wait too); row = the waiting task's row, for the timeout record.
+__device__ __forceinline__ uint32_t gran_settle(FA& a, const uint64_t* p, uint64_t g, int row) {
+  if ((uint32_t)(g >> 32) == a.epoch) return (uint32_t)g;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     __builtin_amdgcn_s_sleep(CAIRO_GRAN_SLEEP);
     g = gran_ld(p);
-    if ((uint32_t)(g >> 32) == tag) break;
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    if ((uint32_t)(g >> 32) == a.epoch) break;
+    if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      report_timeout(a, kWaitGranule, row, (int)a.epoch, (int)((p - a.granules) / kGranuleStride), g);
       break;
     }
   }
@@ -776,7 +794,10 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
       const bool dbr = pv < tagged(a.epoch - back, need) && kDeblock && !kCoderDeblock && kHelperInterleave &&
                        deblock_pending(a, st) && deblock_chunk_ready(a, r, st);
 #endif
-      if (pv >= tagged(a.epoch - back, need)) {
+      if (a.inject && r == min(1, a.hmb - 1)) {  // test hook: this wait "times out" at once
+        report_timeout(a, kWaitInjected, r, need, rr | (back << 16), pv);
+        d = 1;
+      } else if (pv >= tagged(a.epoch - back, need)) {
         d = 1;
       } else if (dbr) {
         d = 2;
@@ -787,8 +808,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
         if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           d = 1;
         } else if (now - t0 > 200000000ull) {
-          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          report_timeout(a, kWaitPrevProgress, r, need, rr | (back << 16), pv);
           d = 1;
         }
       }
@@ -1423,7 +1443,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
         for (int q = 0; q < kDbMBs; q++) {
           if (q >= nmb) break;
           const int m = m0 + q;
-          const uint32_t d = gran_settle(gran_mb(a, m, r) + tid, g[q], a.epoch, a.err, a.sticky);
+          const uint32_t d = gran_settle(a, gran_mb(a, m, r) + tid, g[q], r);
           int pl, row, col;
           if (tid < 128) {
             pl = 0, row = 4 + (tid >> 3), col = m * 16 + 2 * (tid & 7);
@@ -1442,10 +1462,8 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
             if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-              if (tid == kGranulesPerMB) {
-                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              }
+              if (tid == kGranulesPerMB)
+                report_timeout(a, kWaitRowAbove, r, c1, r - 1, progress_at(&prog[r - 1]));
               break;
             }
           }
@@ -1456,7 +1474,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           int e = 0;
           if (row >= 0) {
             const uint64_t* gp = gran_mb(a, m, row) + kGranulesPerMB;
-            e = (int)gran_settle(gp, gran_ld(gp), a.epoch, a.err, a.sticky);
+            e = (int)gran_settle(a, gp, gran_ld(gp), r);
           }
           D.info[t3 & 1][m & 7] = (int16_t)e;
         } else if (r > 0) {  // 4 final rows above: luma 4 x (c1-c0)/2 dwords, chroma 2 x 4 x (c1-c0)/4 (sc1)
@@ -1680,8 +1698,7 @@ __device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbSt
         if (!t0) t0 = now;
         __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
         if (now - t0 > 200000000ull) {
-          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(a.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          report_timeout(a, kWaitRecords, by, a.nref, bx >> 2, (uint32_t)nrec);
           d = 1;
         }
       }
@@ -1927,7 +1944,6 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
   const PlaneSet cs = planes(a.stale);  // the stale rows below (frame index-R)
-  int32_t* err = a.err;
   const uint32_t tag = a.epoch;
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
@@ -1954,7 +1970,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
 #if CAIRO_CODER_DEBLOCK
         coder_wait(a, by, bx, L.db, dst, flag);
 #else
-        if (tid == 0) wait_at_least(&a.inter_done[by * a.ng + (bx >> 2)], a.nref, err, a.sticky);
+        if (tid == 0) wait_records(a, by, bx >> 2);
 #endif
         acquire_after_wait(a.sys);  // the stale rows, references and previous output_cache
       }
@@ -1974,11 +1990,11 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           for (int k = tid; k < n * kGranulesPerMB; k += 256) {
             const int i = k / kGranulesPerMB, kk = k - i * kGranulesPerMB;
             const uint64_t* gp = gran_at(a, lx[i], ly[i], kk);
-            win_put_k(L.win, oy, lx[i], ly[i], kk, gran_settle(gp, gran_ld(gp), tag, err, a.sticky));
+            win_put_k(L.win, oy, lx[i], ly[i], kk, gran_settle(a, gp, gran_ld(gp), by));
           }
         } else if (fresh_col) {
           win_put_k(L.win, oy, bx + 2, by - 1, tid,
-                    gran_settle(fresh_gp, kEarlyGran ? fresh_g : gran_ld(fresh_gp), tag, err, a.sticky));
+                    gran_settle(a, fresh_gp, kEarlyGran ? fresh_g : gran_ld(fresh_gp), by));
         }
       }
       // source rows of this lane's group slot
@@ -2250,10 +2266,10 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       if (tid < kGranulesPerMB) {  // prefetched window blocks for MB bx+1
         if (pf3)
           win_put_k(L.win, oy, bx + 3, by - 3, tid,
-                    gran_settle(gran_at(a, bx + 3, by - 3, tid), pg3, tag, err, a.sticky));
+                    gran_settle(a, gran_at(a, bx + 3, by - 3, tid), pg3, by));
         if (pf2)
           win_put_k(L.win, oy, bx + 3, by - 2, tid,
-                    gran_settle(gran_at(a, bx + 3, by - 2, tid), pg2, tag, err, a.sticky));
+                    gran_settle(a, gran_at(a, bx + 3, by - 2, tid), pg2, by));
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
       if (tid == 0 && !kDecode) a.table[mb] = d;
@@ -2603,6 +2619,8 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   a.granules = e.gran_base + (size_t)f.slot * mbs * kGranuleStride;
   a.err = e.sync + SyncLayout::kErr;
   a.sticky = e.sticky;
+  a.member = f.member;
+  a.inject = e.inject;
   a.ng = (e.wmb + 3) >> 2;
   a.nref = a.inter ? e.ring - 1 : 1;
   a.inter_done = e.sync + SyncLayout::inter_done(e.hmb, a.ng, j);
@@ -2642,8 +2660,8 @@ __global__ __launch_bounds__(64) void k_batch_wait(int32_t* sync, int tasks, int
     __builtin_amdgcn_s_sleep(8);
     if (__hip_atomic_load(sync + SyncLayout::kErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
-      __hip_atomic_store(sync + SyncLayout::kErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      report_timeout(sync + SyncLayout::kErr, sticky, kWaitBatch, 0, -1, -1, -1, tasks, 0,
+                     (uint32_t)__hip_atomic_load(sync + SyncLayout::kDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       break;
     }
   }

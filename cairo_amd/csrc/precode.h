@@ -32,6 +32,12 @@ struct FeedArgs {
   uint32_t* feed;                 // per slot: feed words (device)
   size_t feed_stride;
   uint32_t* hdr;                  // per slot: kFeedHdrWords
+  // k_feed_copy also hands over frame j's block table (table_words uint4 from
+  // its view's table) and the context's timeout words (TimeoutInfo) into
+  // mapped pinned host memory (nullptr: skip)
+  uint4* table_host[kMaxBatch];
+  int32_t* err_host[kMaxBatch];
+  int table_words;
 };
 
 // k_feed_len -> k_feed_scan -> k_feed_write -> k_feed_copy for every frame of a launch.

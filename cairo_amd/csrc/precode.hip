@@ -373,7 +373,11 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
   }
 }
 
-// Phase 4: the used words and the header into the frame's mapped pinned buffer.
+// Phase 4: the used words and the header into the frame's mapped pinned
+// buffer; the frame's block table and the context's timeout words into its
+// mapped pinned stage (what the host entropy stage and the status check read:
+// no per-frame D2H copy, whose shader blit would wait for a workgroup slot of
+// the persistent engine).
 __global__ __launch_bounds__(256) void k_feed_copy(FeedArgs f) {
   const int j = blockIdx.y, slot = f.slot[j];
   const uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
@@ -381,9 +385,16 @@ __global__ __launch_bounds__(256) void k_feed_copy(FeedArgs f) {
   const uint64_t all = (uint64_t)hdr[0] | ((uint64_t)hdr[1] << 32);
   const uint64_t words = hdr[2] ? 0 : (all + 31) / 32;
   const uint32_t* feed = f.feed + (size_t)slot * f.feed_stride;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256)
-    host[kFeedHdrWords + i] = feed[i];
+  const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, di = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = i0; i < words; i += di) host[kFeedHdrWords + i] = feed[i];
   if (blockIdx.x == 0 && threadIdx.x < kFeedHdrWords) host[threadIdx.x] = hdr[threadIdx.x];
+  if (uint4* th = f.table_host[j]) {
+    const uint4* tb = (const uint4*)((FA*)f.fa)[j].table;
+    for (uint64_t i = i0; i < (uint64_t)f.table_words; i += di) th[i] = tb[i];
+  }
+  if (f.err_host[j] && blockIdx.x == 0 && threadIdx.x < TimeoutInfo::kWords)
+    f.err_host[j][threadIdx.x] = __hip_atomic_load(((FA*)f.fa)[j].sticky + threadIdx.x, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace

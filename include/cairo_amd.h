@@ -111,12 +111,15 @@ CAIRO_API int cairo_default_batch(uint32_t width, uint32_t height);
  * previous launch's tasks, merged by the same key with that launch's frames
  * first (no device needed; for tests of the deadlock-freedom argument). */
 CAIRO_API int cairo_task_order(int hmb, int frames, int32_t *out, int *slope);
-/* The per-label queues of a launch of one context (kernels.h kLabels): the
- * same tasks as cairo_task_order, stably partitioned by label, label l's queue
- * being order[seg[l] .. seg[l+1]) (seg: 9 words); *nlab receives 8 on frames
- * of at least 100 macroblock rows (one queue per XCD and pool), else 1 (seg =
- * {0, total, ...}).  No device needed. */
-CAIRO_API int cairo_task_queues(int hmb, int frames, int32_t *order, int32_t *seg, int *nlab);
+/* The queues of one pool (0 row helpers, 1 row coders) of a launch of one
+ * context with n_helpers + n_rows workers (kernels.h kLabels): the same tasks
+ * as cairo_task_order, stably partitioned by label, label l's queue being
+ * order[seg[l] .. seg[l+1]) (seg: 9 words).  *nlab receives 8 where the engine
+ * bands that pool (frames of at least 100 macroblock rows, both worker counts
+ * multiples of 8: one queue per XCD), else 1 (seg = {0, total, ...}) -- the
+ * predicate the launch itself applies.  No device needed. */
+CAIRO_API int cairo_task_queues(int hmb, int frames, int n_helpers, int n_rows, int pool, int32_t *order,
+                                int32_t *seg, int *nlab);
 
 /* Introspection (synchronous; of the last submitted frame).  which: 0 input,
  * 1 output_cache, 2+k ring slot k. */
@@ -137,6 +140,26 @@ CAIRO_API int cairo_ctx_read_stamps(cairo_ctx *ctx, uint64_t *out);
  * in-kernel wait had timed out: every later frame reports
  * EVX_ERROR_HARDWAREFAIL until cairo_ctx_reset. */
 CAIRO_API int cairo_ctx_read_trace(cairo_ctx *ctx, int32_t *out, int n);
+/* flags & 16 (test hook) makes the row helpers of MB row min(1, hmb-1) of
+ * every frame launched from now on record a timeout of their first progress
+ * wait through the device's own reporting path (CAIRO_WAIT_INJECTED), without
+ * waiting; setting flags without 16 clears it. */
+
+/* The in-kernel wait that timed out first, as the last frame that reported
+ * EVX_ERROR_HARDWAREFAIL saw it (zeros: none since create / reset).  Up to 16
+ * int32 words: kind (CAIRO_WAIT_*), the waiting frame's epoch, its stream
+ * index, its MB row, the group member (0 alone), what it needed (columns, a
+ * count or a tag), what it waited on (CAIRO_WAIT_RECORDS: inter group;
+ * _GRANULE: macroblock index; _PREV_PROGRESS / _INJECTED: row | back << 16;
+ * _ROW_ABOVE: row), and the last value it saw (low, high word). */
+#define CAIRO_WAIT_RECORDS 1
+#define CAIRO_WAIT_GRANULE 2
+#define CAIRO_WAIT_PREV_PROGRESS 3
+#define CAIRO_WAIT_ROW_ABOVE 4
+#define CAIRO_WAIT_BATCH 5
+#define CAIRO_WAIT_INJECTED 6
+#define CAIRO_WAIT_HOST_MARK 9
+CAIRO_API int cairo_ctx_timeout_info(cairo_ctx *ctx, int32_t *out, int n);
 CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, int16_t *v);
 
 /* Per-kernel timing (HIP events on the kernels' stream), opt-in. */
@@ -204,10 +227,12 @@ CAIRO_API int cairo_ctx_join_group(cairo_ctx *ctx, int size, int rank, const cai
 /* Whether local_members group members may share one process and device:
  * they need GPU_MAX_HW_QUEUES >= 3 * local_members + 2 (at most 32), or two
  * members' persistent launches can land in one in-order hardware queue and
- * deadlock.  0 = fine (always for fewer than 2), else EVX_ERROR_INVALID_ARGS
- * with a message on stderr.  cairo_ctx_join_group applies it; no device
- * needed. */
-CAIRO_API int cairo_group_check_queues(int local_members);
+ * deadlock.  hw_queues < 0: the process's GPU_MAX_HW_QUEUES as read when the
+ * library was loaded (the HIP runtime reads it once, when it starts: set it
+ * before the process starts; 4 when unset).  0 = fine (always for fewer than
+ * 2), else EVX_ERROR_INVALID_ARGS with a message on stderr.
+ * cairo_ctx_join_group applies it with hw_queues = -1; no device needed. */
+CAIRO_API int cairo_group_check_queues(int local_members, int hw_queues);
 /* Launch the pending (partial) batch now. */
 CAIRO_API int cairo_ctx_flush(cairo_ctx *ctx);
 /* Choose the outputs (CAIRO_OUT_COEF and/or CAIRO_OUT_FEED) for frames

@@ -77,17 +77,32 @@ def test_peek_refuses_other_size(cairo):
 def test_group_queue_check(cairo, monkeypatch):
     """In-process group members on one device need GPU_MAX_HW_QUEUES >= 3N+2
     (backend.hip cairo_group_check_queues; cairo_ctx_join_group applies it):
-    refused with a diagnosis instead of a 2 s in-kernel timeout.  No GPU."""
+    refused with a diagnosis instead of a 2 s in-kernel timeout.  The check
+    uses the value the HIP runtime itself read (the environment when the
+    library was loaded, hw_queues = -1), not one set later.  No GPU."""
     L = cairo.lib()
-    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
-    assert L.cairo_group_check_queues(1) == 0  # one member per process: the production layout
-    assert L.cairo_group_check_queues(2) == 1  # HIP's default 4 < 8
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
-    assert L.cairo_group_check_queues(2) == 0
-    assert L.cairo_group_check_queues(3) == 1
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "32")
-    assert L.cairo_group_check_queues(10) == 0
-    assert L.cairo_group_check_queues(11) == 1  # 35 queues: more than HIP allows
+    assert L.cairo_group_check_queues(1, -1) == 0  # one member per process: the production layout
+    assert L.cairo_group_check_queues(2, 4) == 1  # HIP's default 4 < 8
+    assert L.cairo_group_check_queues(2, 8) == 0
+    assert L.cairo_group_check_queues(3, 8) == 1
+    assert L.cairo_group_check_queues(10, 32) == 0
+    assert L.cairo_group_check_queues(11, 32) == 1  # 35 queues: more than HIP allows
+    loaded = int(os.environ.get("GPU_MAX_HW_QUEUES") or 4)
+    want = 0 if loaded >= 8 else 1
+    assert L.cairo_group_check_queues(2, -1) == want
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "32")  # too late: HIP (and the library) read it at start
+    assert L.cairo_group_check_queues(2, -1) == want
+
+
+def test_timeout_kinds_match_header(cairo):
+    """The timeout record's kinds (kernels.h TimeoutKind) as the header and the
+    binding name them."""
+    text = open(os.path.join(ROOT, "include", "cairo_amd.h")).read()
+    kinds = {int(v): k.lower() for k, v in re.findall(r"#define CAIRO_WAIT_(\w+) (\d+)", text)}
+    assert kinds == cairo.WAIT_KINDS
+    text = open(os.path.join(ROOT, "cairo_amd", "csrc", "kernels.h")).read()
+    dev = {int(v) for v in re.findall(r"kWait\w+ = (\d+)", text)}
+    assert dev == set(kinds)
 
 
 def test_peer_record_size(cairo):

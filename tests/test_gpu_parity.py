@@ -240,7 +240,32 @@ def _payload_bits(cairo, out, ctx, ring, tk):
     return np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[:n]
 
 
-def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None, workgroups=0, outputs=0):
+class _DeviceFrames:
+    """Frames uploaded to HBM before the run (as bench.py keeps them), through
+    the HIP runtime the library itself uses; submitted by device address."""
+
+    def __init__(self, frames):
+        import ctypes
+
+        self.hip = ctypes.CDLL("libamdhip64.so.7")  # by soname: the copy already loaded into this process
+        self.n, self.size = len(frames), frames[0].nbytes
+        self.ptr = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(self.ptr), ctypes.c_size_t(self.n * self.size)) == 0
+        for t, f in enumerate(frames):
+            assert self.hip.hipMemcpy(ctypes.c_void_p(self.ptr.value + t * self.size),
+                                      f.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(self.size), 1) == 0
+
+    def __getitem__(self, t):
+        return self.ptr.value + t * self.size
+
+    def free(self):
+        if self.ptr.value:
+            self.hip.hipFree(self.ptr)
+            self.ptr.value = None
+
+
+def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=None, workgroups=0, outputs=0,
+                 device_frames=False):
     """Frames through one pipelined Context (up to `stages` in flight, `batch`
     frames per launch, 0 = the library default; consecutive launches overlap
     on two streams) vs the oracle: block table and coefficients of every
@@ -248,7 +273,9 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
     set_outputs (0: the default, coefficient planes); with OUT_FEED, as
     bench.py times it, every frame's payload bits (coded from the GPU
     precode's feed) are compared with the oracle's stream record too, and
-    the coefficients are fetched from the staging slot."""
+    the coefficients are fetched from the staging slot.  device_frames: the
+    frames are resident in HBM before the first submit and submitted by
+    device address, as bench.py's timed region does."""
     gen = gen or orc.make_frame
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
@@ -263,6 +290,7 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
         bits = np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[head:nbits]
         ref.append((intra, e.block_table(), e.planes(1), bits))
     final_slots = [e.planes(2 + k) for k in range(ring)]
+    dev = _DeviceFrames([gen(w, h, t) for t in range(frames)]) if device_frames else None
     ctx = cairo.Context(w, h, ring)
     if outputs:
         ctx.set_outputs(outputs)
@@ -291,7 +319,10 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
     for t in range(frames):  # at most `stages` frames in flight (submitted, not released)
         if len(pending) == stages:
             check(*pending.pop(0))
-        pending.append((t, ctx.submit(gen(w, h, t), t, not ref[t][0], q)))
+        if dev is not None:
+            pending.append((t, ctx.submit(dev[t], t, not ref[t][0], q, on_device=True)))
+        else:
+            pending.append((t, ctx.submit(gen(w, h, t), t, not ref[t][0], q)))
     for p in pending:
         check(*p)
     ctx.sync()
@@ -301,6 +332,8 @@ def _run_batched(orc, cairo, w, h, ring, q, frames, batch, intra_every=0, gen=No
         np.testing.assert_array_equal(gu, final_slots[k][1], err_msg=f"slot {k} U")
         np.testing.assert_array_equal(gv, final_slots[k][2], err_msg=f"slot {k} V")
     ctx.close()
+    if dev is not None:
+        dev.free()
 
 
 @pytest.mark.parametrize("ring,batch", [(2, 8), (4, 8), (3, 5), (2, 1)])

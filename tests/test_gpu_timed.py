@@ -53,16 +53,27 @@ def test_timed_4k_default_batch(orc, cairo):
     _run_batched(orc, cairo, 3840, 2160, 4, 16, 31, 0, outputs=cairo.OUT_FEED)
 
 
+def test_timed_4k_many_launches(orc, cairo):
+    """configs[3] past the first launches: 4K q=16 R=4 with the bench's
+    banded queues, helper priority, feed outputs and device-resident frames,
+    10 frames per launch, 44 frames = 5 launches.  Launch b reuses the sync
+    area, task queue and frame views of launch b-3 (backend.hip flush: areas
+    rotate mod 3) while launch b-1 still runs beside it, so launches 3 and 4
+    run on recycled state; every frame's payload bits, block table and
+    coefficients and every ring slot at the end against the oracle."""
+    _run_batched(orc, cairo, 3840, 2160, 4, 16, 44, 10, outputs=cairo.OUT_FEED, device_frames=True)
+
+
 def test_timed_4k_both_outputs(orc, cairo):
     """The same launches with both outputs (coefficient planes D2H and the
     feed): 4K, 6 frames."""
     _run_batched(orc, cairo, 3840, 2160, 4, 16, 6, 0, outputs=cairo.OUT_FEED | cairo.OUT_COEF)
 
 
-@pytest.mark.parametrize("q,frames", [(1, 31), (8, 3), (31, 31)])
+@pytest.mark.parametrize("q,frames", [(1, 31), (8, 31), (31, 31)])
 def test_4k_quality_sweep(orc, cairo, q, frames):
     """configs[4]: the 4K quality sweep (VAQ on), default launch, feed
-    outputs.  q = 1 and 31 (the ends of the sweep) over 31 frames: two
+    outputs.  q = 1 and 31 (the ends of the sweep) and 8 over 31 frames: two
     overlapping 28-frame launches, every payload against the oracle."""
     _run_batched(orc, cairo, 3840, 2160, 4, q, frames, 0, outputs=cairo.OUT_FEED)
 
@@ -204,17 +215,39 @@ def test_peek_views(orc, cairo):
 
 
 def test_reset_recovers_after_timeout(orc, cairo):
-    """A reported in-kernel timeout (the sticky word, set here by the test
-    hook) fails every frame until cairo_ctx_reset, which restores a
-    fresh-encoder state (common.cpp:79-150): the next stream is bit-exact."""
+    """A reported in-kernel timeout fails every frame until cairo_ctx_reset,
+    which restores a fresh-encoder state (common.cpp:79-150): the next stream
+    is bit-exact.  The report names the wait: first the host's mark (test
+    hook 8), then a row helper's progress wait recorded by the device's own
+    timeout path (test hook 16): kind, frame epoch and index, MB row,
+    member, the awaited row, the columns it needed."""
     w, h, ring, q = 352, 288, 2, 16
     ctx = cairo.Context(w, h, ring)
+    assert ctx.timeout_info() is None
     ctx.encode_frame(orc.make_frame(w, h, 0), 0, False, q)
     ctx.set_debug(8)
     with pytest.raises(cairo.CairoError) as ei:
         ctx.encode_frame(orc.make_frame(w, h, 1), 1, True, q)
     assert ei.value.status == cairo.EVX_ERROR_HARDWAREFAIL
+    assert ei.value.timeout["kind"] == "host_mark"
     cairo.lib().cairo_ctx_reset(ctx.h)
+    assert ctx.timeout_info() is None
+    ctx.encode_frame(orc.make_frame(w, h, 0), 0, False, q)  # epoch 1
+    ctx.set_debug(16)
+    with pytest.raises(cairo.CairoError) as ei:
+        ctx.encode_frame(orc.make_frame(w, h, 1), 1, True, q)  # epoch 2
+    assert ei.value.status == cairo.EVX_ERROR_HARDWAREFAIL
+    info = ctx.timeout_info()
+    assert info == ei.value.timeout
+    # row 1's helper, its first wait: frame index-2 is none yet at frame 1
+    # (R = 2: no older reference), so the previous frame's progress of row
+    # min(r + 2, hmb - 1) = 3 at the level-1 window of group 0 (80 columns)
+    assert info["kind"] == "injected" and info["member"] == 0
+    assert (info["epoch"], info["index"], info["row"]) == (2, 1, 1)
+    assert (info["on"] & 0xFFFF, info["on"] >> 16, info["need"]) == (3, 1, 80)
+    ctx.set_debug(0)
+    cairo.lib().cairo_ctx_reset(ctx.h)
+    assert ctx.timeout_info() is None
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
     for t in range(3):

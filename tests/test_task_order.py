@@ -99,6 +99,9 @@ def test_label_queues_partition_the_order(cairo, hmb):
         o, slope = cairo.task_order(hmb, frames)
         q, seg, nlab = cairo.task_queues(hmb, frames)
         assert nlab == (8 if hmb >= 100 else 1)
+        # the launch's own predicate: both worker counts split over the 8 labels
+        assert cairo.task_queues(hmb, frames, helpers=191, rows=193)[2] == 1
+        assert cairo.task_queues(hmb, frames, helpers=96, rows=96, pool=1)[2] == nlab
         assert seg[0] == 0 and list(seg) == sorted(seg) and seg[nlab] == frames * hmb
         assert all(seg[l] == frames * hmb for l in range(nlab, 9))
         lab_of = lambda x: (int(x) & 0xFFFF) * 8 // hmb if nlab == 8 else 0

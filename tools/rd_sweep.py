@@ -56,7 +56,8 @@ def main():
     ap.add_argument("--frames", type=int, default=160, help="timed P-frames per quality")
     ap.add_argument("--q", default="1,2,4,8,12,16,20,24,28,31")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rd_sweep.json"))
-    ap.add_argument("--check", type=int, default=3, help="frames per quality pinned by their record hashes")
+    ap.add_argument("--check", type=int, default=8,
+                    help="frames per quality pinned by their record hashes (SURVEY §8(d) Config 5: >= 8)")
     a = ap.parse_args()
     import torch
 
