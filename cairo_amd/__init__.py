@@ -102,6 +102,7 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_join_group": (I, [P, I, I, P]),
         "cairo_group_check_queues": (I, [I, I]),
         "cairo_ctx_timeout_info": (I, [P, P, I]),
+        "cairo_ctx_read_acct": (I, [P, P, I, I]),
         "cairo_peer_size": (I, []),
         "cairo_ctx_flush": (I, [P]),
         "cairo_ctx_set_helpers": (I, [P, I]),
@@ -268,6 +269,17 @@ class Context:
             raise CairoError("cairo_ctx_wait", st, self.timeout_info() if st == EVX_ERROR_HARDWAREFAIL else None)
         self._keep.pop(ticket, None)
         return self._outputs(r, copy)
+
+    ACCT_FIELDS = ("coder_tasks", "coder_total", "coder_group_wait", "coder_window", "coder_search", "coder_inter",
+                   "coder_dequeue", "coder_mbs", "helper_tasks", "helper_total", "helper_wait", "helper_deblock",
+                   "helper_search", "helper_catchup", "helper_dequeue", "helper_chunks")
+
+    def read_acct(self, reset: bool = False) -> dict:
+        """Engine time accounting (set_debug(32) on a CAIRO_ACCT=1 build): 10 ns
+        ticks per role and phase summed over all tasks (kernels.h Acct)."""
+        w = np.zeros(16, np.uint64)
+        _ck(self.L.cairo_ctx_read_acct(self.h, _ptr(w), 16, int(reset)), "cairo_ctx_read_acct")
+        return {k: int(w[i]) for i, k in enumerate(self.ACCT_FIELDS)}
 
     def timeout_info(self) -> dict | None:
         """The in-kernel wait that timed out first, as last reported

@@ -214,6 +214,7 @@ struct cairo_ctx {
   std::vector<std::pair<double, double>> busy;  // engine [start, end) per launch, ms after t_base
   int16_t* predeblock = nullptr;  // debug: pre-deblock reconstruction of the last frame (opt-in)
   uint64_t* stamps = nullptr;     // diagnostic phase stamps (opt-in)
+  uint64_t* acct = nullptr;       // diagnostic time accounting (opt-in; CAIRO_ACCT builds fill it)
   // Thread safety (the frame pipeline of pipeline.cpp calls in from its
   // completion and entropy threads): every public entry point holds mu;
   // HIP event waits on a frame's outputs run outside it.  launched_cv is
@@ -306,6 +307,7 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.sticky = c->sticky;
   e.inject = c->inject;
   e.stamps = c->stamps;
+  e.acct = c->acct;
   e.trace = c->trace_dev;
   return e;
 }
@@ -434,7 +436,7 @@ void free_ctx(cairo_ctx* c) {
     if (q) (void)hipFree(q);
   for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress, (void*)c->feed_dev, (void*)c->feed_hdr, (void*)c->feed_scratch,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
-                  (void*)c->predeblock, (void*)c->stamps})
+                  (void*)c->predeblock, (void*)c->stamps, (void*)c->acct})
     (void)hipFree(p);
   if (c->us) (void)hipStreamSynchronize(c->us);
   if (c->up_last) (void)hipEventDestroy(c->up_last);
@@ -1532,6 +1534,18 @@ int cairo_ctx_read_inter(cairo_ctx* c, uint8_t* descs, int32_t* sads) {
   const size_t n = c->mbs * (c->ring > 1 ? c->ring - 1 : 0);
   if (!n) return kSuccess;
   const size_t o = (size_t)c->last_slot * c->nref * c->mbs;
+  if (CAIRO_TAGGED_RECORDS) {  // two tagged granules per record (kernels.h pack_inter_desc)
+    std::vector<uint64_t> g(2 * n);
+    CK(hipMemcpy(g.data(), c->idesc + o, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; i++) {
+      if (descs) {
+        const BlockDesc d = unpack_inter_desc((uint32_t)g[2 * i]);
+        memcpy(descs + i * sizeof(BlockDesc), &d, sizeof(d));
+      }
+      if (sads) sads[i] = (int32_t)(uint32_t)g[2 * i + 1];
+    }
+    return kSuccess;
+  }
   if (descs) CK(hipMemcpy(descs, c->idesc + o, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
   if (sads) CK(hipMemcpy(sads, c->isad + o, n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return kSuccess;
@@ -1555,6 +1569,26 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
     CK(hipMemcpy(c->sticky, &mark, sizeof(mark), hipMemcpyHostToDevice));
   }
   c->inject = (flags & 16) ? 1 : 0;
+  if ((flags & 32) && !c->acct) {
+    CK(hipMalloc(&c->acct, kAcctShards * kAcctWords * sizeof(uint64_t)));
+    CK(hipMemset(c->acct, 0, kAcctShards * kAcctWords * sizeof(uint64_t)));
+  }
+  return kSuccess;
+}
+
+int cairo_ctx_read_acct(cairo_ctx* c, uint64_t* out, int n, int reset) {
+  if (!c || !out || n < 0 || n > kAcctWords) return kInvalidArg;
+  std::lock_guard<std::mutex> lk(c->mu);
+  memset(out, 0, (size_t)n * sizeof(uint64_t));
+  if (!c->acct) return kSuccess;
+  CK(hipSetDevice(c->device));
+  int r = sync_all(c);
+  if (r) return r;
+  std::vector<uint64_t> v((size_t)kAcctShards * kAcctWords);
+  CK(hipMemcpy(v.data(), c->acct, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  for (int s = 0; s < kAcctShards; s++)
+    for (int k = 0; k < n; k++) out[k] += v[(size_t)s * kAcctWords + k];
+  if (reset) CK(hipMemset(c->acct, 0, v.size() * sizeof(uint64_t)));
   return kSuccess;
 }
 

@@ -33,6 +33,37 @@ __host__ __device__ inline PlaneSet ring_slot(int16_t* base, size_t slot_elems, 
 constexpr int kGranulesPerMB = 192;   // pixel granules
 constexpr int kGranuleStride = 193;   // + info granule
 
+// Inter-search records (one per macroblock and reference offset) as two
+// tagged granules in the 16 bytes of an evx_block_desc slot: {epoch, packed
+// desc} and {epoch, SAD}.  The row coder polls them by tag (no drain and no
+// counter on the helper's side).  The packed desc holds what an inter record
+// can carry: type (3 bits), target (2), sp_pred, sp_amount, sp_index (4), and
+// the motion vector (7 bits each: |mv| <= 31, the search's reach).
+// CAIRO_TAGGED_RECORDS 0: plain stores the helper drains before counting
+// them in inter_done (the round-3 form, kept for A/B timing).
+#ifndef CAIRO_TAGGED_RECORDS
+#define CAIRO_TAGGED_RECORDS 1
+#endif
+__host__ __device__ inline uint32_t pack_inter_desc(const BlockDesc& d) {
+  return (d.block_type & 7u) | ((uint32_t)(d.prediction_target & 3) << 3) | ((uint32_t)(d.sp_pred & 1) << 5) |
+         ((uint32_t)(d.sp_amount & 1) << 6) | ((uint32_t)(d.sp_index & 15) << 7) |
+         (((uint32_t)d.motion_x & 0x7Fu) << 11) | (((uint32_t)d.motion_y & 0x7Fu) << 18);
+}
+__host__ __device__ inline BlockDesc unpack_inter_desc(uint32_t w) {
+  BlockDesc d;
+  d.block_type = w & 7u;
+  d.prediction_target = (uint8_t)((w >> 3) & 3);
+  d.pad = 0;
+  d.sp_pred = (uint8_t)((w >> 5) & 1);
+  d.sp_amount = (uint8_t)((w >> 6) & 1);
+  d.sp_index = (uint8_t)((w >> 7) & 15);
+  d.motion_x = (int16_t)((int32_t)(w << 14) >> 25);  // bits 11..17, sign-extended
+  d.motion_y = (int16_t)((int32_t)(w << 7) >> 25);   // bits 18..24
+  d.q_index = 0;
+  d.variance = 0;
+  return d;
+}
+
 // Phase boundaries recorded per macroblock by the row code when stamps != nullptr.
 constexpr int kStampPhases = 12;  // 10 real-time stamps + 2 shader-clock stamps
 // ...followed by kDbStamps per MB row: the deblock's publish time of each
@@ -74,6 +105,21 @@ enum TimeoutKind : int32_t {
   kWaitInjected = 6,      // test hook (cairo_ctx_set_debug 16): a helper's progress wait,
                           // recorded as kWaitPrevProgress would be, without waiting
   kWaitHostMark = 9,      // test hook (cairo_ctx_set_debug 8): marked by the host
+};
+
+// Time accounting (CAIRO_ACCT=1 builds, cairo_ctx_set_debug 32): where the
+// workers' time goes in the steady state, summed over all tasks.
+#ifndef CAIRO_ACCT
+#define CAIRO_ACCT 0
+#endif
+constexpr int kAcctShards = 64, kAcctWords = 16;
+struct Acct {
+  // row coders
+  static constexpr int kCoderTasks = 0, kCoderTotal = 1, kCoderGroupWait = 2, kCoderWindow = 3, kCoderSearch = 4,
+                       kCoderInter = 5, kCoderDequeue = 6, kCoderMBs = 7;
+  // row helpers
+  static constexpr int kHelperTasks = 8, kHelperTotal = 9, kHelperWait = 10, kHelperDeblock = 11, kHelperSearch = 12,
+                       kHelperCatchup = 13, kHelperDequeue = 14, kHelperChunks = 15;
 };
 
 // Frames per engine launch.
@@ -172,6 +218,7 @@ struct FrameArgs {
   int sys;
   int db_shift;        // deblock chunk width, log2 luma columns (4..6: 1, 2 or 4 macroblocks)
   uint64_t* stamps;    // diagnostic (nullptr = off)
+  uint64_t* acct;      // diagnostic time accounting (EngineArgs::acct)
   uint64_t* istamps;   // diagnostic: per (row, group) of the inter search, kIStamps stamps (see kernels.hip)
   const uint8_t* rgb;  // RGB888 input, pitch 3*w (device memory)
 };
@@ -211,6 +258,10 @@ struct EngineArgs {
   int32_t* sticky;         // TimeoutInfo words
   int inject;              // FrameArgs::inject
   uint64_t* stamps;
+  // Diagnostic time accounting of a build with CAIRO_ACCT=1 (nullptr = off):
+  // [kAcctShards][kAcctWords] u64, 10 ns ticks summed per role and phase over
+  // every task of the steady state (Acct), sharded by workgroup index.
+  uint64_t* acct;
   int n_helpers, n_rows;   // worker pools (workgroups), spread over the block indices (is_helper)
   int32_t* trace;          // diagnostic: [blockIdx][4] live state in mapped host memory (nullptr = off)
   // Per pool (0 helpers, 1 row coders): [nframes * hmb] task order, (frame << 16 | row)

@@ -173,6 +173,15 @@ __device__ __forceinline__ void stamp(FA& a, int mb, int k) {
     a.stamps[(size_t)mb * kStampPhases + k] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Time accounting (kernels.h Acct; CAIRO_ACCT=1 builds with cairo_ctx_set_debug
+// 32): thread 0 adds 10 ns ticks to its workgroup's shard (posted atomics).
+__device__ __forceinline__ uint64_t acct_now() { return CAIRO_ACCT ? __builtin_amdgcn_s_memrealtime() : 0; }
+__device__ __forceinline__ void acct_add(uint64_t* acct, int k, uint64_t v) {
+  if (CAIRO_ACCT && acct && threadIdx.x == 0)
+    __hip_atomic_fetch_add(&acct[(blockIdx.x & (kAcctShards - 1)) * kAcctWords + k], v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Deblock progress words (kernels.h FrameArgs::progress): tag a column count
 // with the frame's epoch; relaxed agent-scope 64-bit loads.
 __device__ __forceinline__ uint64_t tagged(uint32_t epoch, int cols) {
@@ -268,6 +277,25 @@ __device__ __forceinline__ uint64_t gran_ld(const uint64_t* p) {
 __device__ __forceinline__ void gran_st(uint64_t* p, uint64_t v) {
   __hip_atomic_store((gbl_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The record granule p of frame a (tagged inter records, kernels.h
+// pack_inter_desc), given a first load g: re-polls until the tag is the
+// frame's epoch; bounded (report_timeout: kind records, on = the macroblock).
+__device__ __forceinline__ uint32_t rec_settle(FA& a, const uint64_t* p, uint64_t g, int row, int mb) {
+  if ((uint32_t)(g >> 32) == a.epoch) return (uint32_t)g;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
+    g = gran_ld(p);
+    if ((uint32_t)(g >> 32) == a.epoch) break;
+    if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+      report_timeout(a, kWaitRecords, row, (int)a.epoch, mb, g);
+      break;
+    }
+  }
+  return (uint32_t)g;
+}
+
 // Data of granule p of frame a, given a first load g: re-polls until the tag
 // is the frame's epoch.  Bounded like every wait (the error word ends every
 // other wait too); row = the waiting task's row, for the timeout record.
@@ -455,6 +483,76 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
         }
       }
   }
+}
+
+// The same staging by LDS-DMA (global_load_lds: no VGPR destination, so every
+// load of the window is in flight at once -- one fabric round trip instead of
+// one per kWinUnroll loads), then an in-LDS pass that biases the staged
+// region.  One wave instruction stages one window row: luma 64 lanes x 4 B
+// (128 columns, pitch kWinLP), chroma 64 lanes x 2 B (64 columns, pitch
+// kWinCP): an LDS-DMA writes wave-uniform base + lane x size, so each row's
+// padding stays outside.  Rows outside the frame are skipped; lanes whose
+// columns fall outside [c0, c1) or the frame are masked off.  All 256 threads
+// participate; ends with the bias pass's writes issued (the caller's barrier
+// publishes them).
+#ifndef CAIRO_WIN_DMA
+#define CAIRO_WIN_DMA 1
+#endif
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
+                                                int r1, int c0, int c1) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  {  // luma: rows r0 + wave, r0 + wave + 4, ...; lane = column pair
+    const int c = 2 * lane, gx = ox + c;
+    const bool col_ok = c >= c0 && c < c1 && gx >= 0 && gx < wa;
+    for (int r = r0 + wave; r < r1; r += 4) {
+      const int gy = oy + r;
+      if (gy < 0 || gy >= ha) continue;  // wave-uniform
+      if (col_ok)
+        __builtin_amdgcn_global_load_lds((const void*)&p.y[(size_t)gy * wa + gx], (lds_void*)&w.y[r * kWinLP], 4, 0, 0);
+    }
+  }
+  {  // chroma: U rows then V rows, [r0/2, r1/2); lane = column
+    const int cr0 = r0 >> 1, cr1 = r1 >> 1, ncr = cr1 - cr0;
+    const int cw = wa >> 1, ch = ha >> 1, cx = lane, gx = (ox >> 1) + cx;
+    const bool col_ok = 2 * cx >= c0 && 2 * cx < c1 && gx >= 0 && gx < cw;
+    for (int k = wave; k < 2 * ncr; k += 4) {
+      const int pl = k >= ncr, r = cr0 + k - (pl ? ncr : 0), gy = (oy >> 1) + r;
+      if (gy < 0 || gy >= ch) continue;
+      if (col_ok)
+        __builtin_amdgcn_global_load_lds((const void*)&pick(p, 1 + pl)[(size_t)gy * cw + gx],
+                                         (lds_void*)&(pl ? w.v : w.u)[r * kWinCP], 2, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
+  __syncthreads();                                    // ... every wave's
+  // bias the staged region (v ^ 0x8000) in 16-byte chunks: luma 16 lanes per
+  // row (8 columns each), chroma 8 lanes per row
+  {
+    const int k0 = c0 >> 3, k1 = c1 >> 3;  // luma chunks of the staged columns
+    const int rr = lane >> 4, kk = lane & 15;
+    if (kk >= k0 && kk < k1)
+      for (int r = r0 + 4 * wave + rr; r < r1; r += 16) {
+        uint4* q = (uint4*)&w.y[r * kWinLP + 8 * kk];
+        *q = bias4(*q);
+      }
+    const int cr0 = r0 >> 1, cr1 = r1 >> 1, ck0 = c0 >> 4, ck1 = c1 >> 4;
+    const int crr = lane >> 3, ckk = lane & 7;
+    if (ckk >= ck0 && ckk < ck1)
+      for (int k = 8 * wave + crr; k < 2 * (cr1 - cr0); k += 32) {
+        const int pl = k >= cr1 - cr0, r = cr0 + k - (pl ? cr1 - cr0 : 0);
+        uint4* q = (uint4*)&(pl ? w.v : w.u)[r * kWinCP + 8 * ckk];
+        *q = bias4(*q);
+      }
+  }
+}
+
+__device__ __forceinline__ void stage_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
+                                             int r1, int c0, int c1) {
+  if (CAIRO_WIN_DMA)
+    load_window_dma(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
+  else
+    load_window(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
 }
 
 // Per-lane slice of a macroblock: luma row l>>2, columns (l&3)*4..+3, and the
@@ -753,6 +851,9 @@ constexpr bool kHelperInterleave = CAIRO_HELPER_INTERLEAVE;
 #define CAIRO_CODER_DEBLOCK 0
 #endif
 constexpr bool kCoderDeblock = CAIRO_CODER_DEBLOCK;
+// Inter records as tagged granules (kernels.h CAIRO_TAGGED_RECORDS).
+constexpr bool kTaggedRecords = CAIRO_TAGGED_RECORDS && !CAIRO_CODER_DEBLOCK;
+static_assert(!(CAIRO_TAGGED_RECORDS && CAIRO_CODER_DEBLOCK), "the coder-side deblock waits on inter_done");
 
 // Thread 0's value v, broadcast to the workgroup (two barriers).
 __device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
@@ -781,6 +882,8 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
   volatile int* vflag = flag;
   const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
   uint64_t t0 = 0;
+  const uint64_t ta = acct_now();
+  uint64_t tdb = 0;  // accounting: time in deblock chunks run here
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
@@ -815,13 +918,18 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
     }
     d = wg_broadcast(vflag, d);
     if (d == 1) break;
-    if (kDeblock && d == 2) deblock_chunk(a, r, D, st, true);
+    if (kDeblock && d == 2) {
+      const uint64_t tb = acct_now();
+      deblock_chunk(a, r, D, st, true);
+      tdb += acct_now() - tb;
+    }
   }
   if (threadIdx.x == 0) {  // the check used a relaxed load: acquire what it observed
     acquire_fence(a.sys);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  acct_add(a.acct, Acct::kHelperWait, acct_now() - ta - tdb);
 }
 
 #ifndef CAIRO_DB_IN_WAIT1
@@ -976,7 +1084,7 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
     const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
     const bool full = L.full != 0;  // workgroup-uniform
-    load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
+    stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     __syncthreads();
     if (is && off == 1) is[4] = __builtin_amdgcn_s_memrealtime();
     bool lvl2c = full, lvl2r = full;  // workgroup-uniform
@@ -1005,8 +1113,8 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
           // the search state live here)
           helper_wait<false>(a, off == 1 ? 1 : 2, r, min(r + ((m & 2) ? 3 : 2), a.hmb - 1), inter_need_cols(a, g, 2),
                              D, st, flag);
-          if (m & 2) load_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
-          if (!lvl2c) load_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
+          if (m & 2) stage_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
+          if (!lvl2c) stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
           __syncthreads();
           if (is) is[6] = __builtin_amdgcn_s_memrealtime(), is[7] += (m & 2) ? 0x10000 : 1;
           lvl2c = true;
@@ -1108,20 +1216,29 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   }
   if (is && off == 1) is[10] = __builtin_amdgcn_s_memrealtime();
   if (valid && (threadIdx.x & 63) == 0) {
-    // Write-through (sc1) stores: complete at the coherence point once vmcnt
-    // drains, so the counter below is published without a release fence,
-    // whose L2 write-back (buffer_wbl2) per reference and group cost 9 % at
-    // 4K (MI355X_MICROARCH.md R2; the coder acquires after its wait).
     const BlockDesc d = make_desc(s, px, py, thr, false, off);
-    uint32_t wd[4];
-    memcpy(wd, &d, sizeof(wd));
-    gbl_u32* dst = (gbl_u32*)&a.inter_desc[(off - 1) * mbs + mb];
+    if (kTaggedRecords) {
+      // two tagged granules (kernels.h pack_inter_desc): the coder polls them,
+      // so nothing waits for these stores
+      uint64_t* rec = (uint64_t*)&a.inter_desc[(off - 1) * mbs + mb];
+      const uint64_t tag = (uint64_t)a.epoch << 32;
+      gran_st(rec, tag | pack_inter_desc(d));
+      gran_st(rec + 1, tag | (uint32_t)s.sad);
+    } else {
+      // Write-through (sc1) stores: complete at the coherence point once vmcnt
+      // drains, so the counter below is published without a release fence,
+      // whose L2 write-back (buffer_wbl2) per reference and group cost 9 % at
+      // 4K (MI355X_MICROARCH.md R2; the coder acquires after its wait).
+      uint32_t wd[4];
+      memcpy(wd, &d, sizeof(wd));
+      gbl_u32* dst = (gbl_u32*)&a.inter_desc[(off - 1) * mbs + mb];
 #pragma unroll
-    for (int k = 0; k < 4; k++) __hip_atomic_store(dst + k, wd[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gbl_u32*)&a.inter_sad[(off - 1) * mbs + mb], (uint32_t)s.sad, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < 4; k++) __hip_atomic_store(dst + k, wd[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gbl_u32*)&a.inter_sad[(off - 1) * mbs + mb], (uint32_t)s.sad, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  if (publish) {
+  if (publish && !kTaggedRecords) {
     // all records of the group's tasks stored (vmcnt counts every store of
     // the wave, earlier tasks' included); release them to the row coder
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1415,6 +1532,7 @@ __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState&
 __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st, bool known_ready) {
   const int tid = threadIdx.x;
   const uint64_t tb = a.stamps && tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint64_t ta = acct_now();
   const PlaneSet cs = planes(a.recon[0]);
   const int cw = a.wa >> 1;
   const int y0 = 16 * r - 4, c0y = 8 * r - 4;  // tile origins (pixel rows)
@@ -1612,6 +1730,8 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
   }
   st.k++;
   if (tb) st.busy += __builtin_amdgcn_s_memrealtime() - tb;
+  acct_add(a.acct, Acct::kHelperDeblock, acct_now() - ta);
+  acct_add(a.acct, Acct::kHelperChunks, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1663,6 +1783,12 @@ struct alignas(16) RowLds {
 #define CAIRO_EARLY_GRAN 1
 #endif
 constexpr bool kEarlyGran = CAIRO_EARLY_GRAN;
+// At a group start, the intra search before the wait for the group's inter
+// records (1) or after it (0).
+#ifndef CAIRO_SEARCH_FIRST
+#define CAIRO_SEARCH_FIRST 1
+#endif
+constexpr bool kSearchFirst = CAIRO_SEARCH_FIRST;
 
 // Deblock chunks the coder may leave pending at a group start before it runs
 // a ready one even when its inter records are already there (the next
@@ -1966,14 +2092,42 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       const bool fresh_col = by > 0 && bx != 0 && bx + 2 < a.wmb && tid < kGranulesPerMB;
       const uint64_t* fresh_gp = fresh_col ? gran_at(a, bx + 2, by - 1, tid) : nullptr;
       const uint64_t fresh_g = (kEarlyGran && fresh_col) ? gran_ld(fresh_gp) : 0;
-      if ((bx & 3) == 0) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
+      // At a group start the coder needs the group's inter records, and every
+      // cross-frame dependency they carry (the stale rows, references and
+      // previous output_cache), only for the classification: the intra search
+      // reads nothing but the LDS window.  So it runs first (early), while the
+      // records may still be on their way; the acquire, when the records are
+      // already in, completes behind it (it issues no vector-memory access).
+      const bool gstart = (bx & 3) == 0;
+      const bool early = kSearchFirst && !kDecode && !kCoderDeblock && gstart;  // workgroup-uniform
+      uint64_t tacc = acct_now();
+      // thread 0: one poll of the group's record count, issued with the fresh
+      // granule load and tested after the window update (which waits for it anyway)
+      // With tagged records (inter frames) the group is ready once its first
+      // macroblock's record of reference 1 -- the helper's last search, after
+      // its wait for the previous frame -- carries this frame's tag; otherwise
+      // (intra and decoded frames: the helper's carrier) once inter_done says so.
+      const bool by_tag = kTaggedRecords && a.inter;  // workgroup-uniform
+      const uint64_t* grec = (const uint64_t*)&a.inter_desc[mb];  // reference 1, this MB
+      uint64_t rd0 = 0;
+      if (early && tid == 0)
+        rd0 = by_tag ? gran_ld(grec)
+                     : (uint64_t)__hip_atomic_load(&a.inter_done[by * a.ng + (bx >> 2)], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      bool ready0 = false;  // thread 0: the records were in before the search
+      if (gstart && !early) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
 #if CAIRO_CODER_DEBLOCK
         coder_wait(a, by, bx, L.db, dst, flag);
 #else
-        if (tid == 0) wait_records(a, by, bx >> 2);
+        if (tid == 0) {
+          if (by_tag) rec_settle(a, grec, gran_ld(grec), by, mb);
+          else wait_records(a, by, bx >> 2);
+        }
 #endif
         acquire_after_wait(a.sys);  // the stale rows, references and previous output_cache
+        acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
       }
+      tacc = acct_now();
 
       // ---- window.  Reconstruction of the rows above arrives as granules
       //      (this frame's data, polled by tag); the stale row below is the
@@ -1997,6 +2151,11 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
                     gran_settle(a, fresh_gp, kEarlyGran ? fresh_g : gran_ld(fresh_gp), by));
         }
       }
+      acct_add(a.acct, Acct::kCoderWindow, acct_now() - tacc);
+      if (early && tid == 0) {
+        ready0 = by_tag ? (uint32_t)(rd0 >> 32) == a.epoch : (int)rd0 >= a.nref;
+        if (ready0) acquire_fence(a.sys);  // completes during the search; waited for after it
+      }
       // source rows of this lane's group slot
       SrcRow s;  // biased u16 pairs (the encoder's source; unused when decoding)
       if (!kDecode) {
@@ -2019,7 +2178,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       if (tid < kGranulesPerMB) {
         if (pf3) pg3 = gran_ld(gran_at(a, bx + 3, by - 3, tid));
         if (pf2) pg2 = gran_ld(gran_at(a, bx + 3, by - 2, tid));
-        if (pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);
+        if (pfs && !early) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);  // (early: after the wait)
       }
 
       // ---- inter predictions, prefetched (the K1 records are final) ----
@@ -2027,31 +2186,59 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       int inter_sad[kMaxRing - 1];
       int ipv[kMaxRing - 1][2];
       const int nref = a.inter ? a.ring - 1 : 0;
-      uint4 idw[kMaxRing - 1];  // all records' loads issued before the first wait
-      int isw[kMaxRing - 1];
+      auto load_inter = [&]() {
+        if (kTaggedRecords) {
+          // each wave loads the macroblock's 2 * nref record granules (every
+          // lane the same addresses), all issued before the first is tested
+          uint64_t rg[kMaxRing - 1][2];
 #pragma unroll
-      for (int o = 0; o < kMaxRing - 1; o++) {
-        if (o >= nref) break;
-        idw[o] = *(const uint4*)&a.inter_desc[o * mbs + mb];
-        isw[o] = a.inter_sad[o * mbs + mb];
-      }
+          for (int o = 0; o < kMaxRing - 1; o++) {
+            if (o >= nref) break;
+            const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
+            rg[o][0] = gran_ld(r);
+            rg[o][1] = gran_ld(r + 1);
+          }
 #pragma unroll
-      for (int o = 0; o < kMaxRing - 1; o++) {
-        if (o >= nref) break;
-        inter_d[o] = uni_desc_words(idw[o]);
-        inter_sad[o] = uni(isw[o]);
-        const BlockDesc& d = inter_d[o];
-        const PlaneSet rp = RECON_AT(a, d.prediction_target);
-        const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
-        int dx = 0, dy = 0;
-        if (sp) frac_dir(d.sp_index, &dx, &dy);
-        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
-          ipv[o][bi] = pred_global(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
-                                   py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
-      }
+          for (int o = 0; o < kMaxRing - 1; o++) {
+            if (o >= nref) break;
+            const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
+            inter_d[o] = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
+            inter_sad[o] = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
+          }
+        } else {
+          uint4 idw[kMaxRing - 1];  // all records' loads issued before the first wait
+          int isw[kMaxRing - 1];
+#pragma unroll
+          for (int o = 0; o < kMaxRing - 1; o++) {
+            if (o >= nref) break;
+            idw[o] = *(const uint4*)&a.inter_desc[o * mbs + mb];
+            isw[o] = a.inter_sad[o * mbs + mb];
+          }
+#pragma unroll
+          for (int o = 0; o < kMaxRing - 1; o++) {
+            if (o >= nref) break;
+            inter_d[o] = uni_desc_words(idw[o]);
+            inter_sad[o] = uni(isw[o]);
+          }
+        }
+#pragma unroll
+        for (int o = 0; o < kMaxRing - 1; o++) {
+          if (o >= nref) break;
+          const BlockDesc& d = inter_d[o];
+          const PlaneSet rp = RECON_AT(a, d.prediction_target);
+          const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
+          int dx = 0, dy = 0;
+          if (sp) frac_dir(d.sp_index, &dx, &dy);
+          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
+            ipv[o][bi] = pred_global(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
+                                     py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
+        }
+      };
+      if (!early) load_inter();
       stamp(a, mb, 1);
       __syncthreads();
       stamp(a, mb, 2);
+      tacc = acct_now();
 
       BlockDesc d;
       bool from_inter = false;  // an inter record won / an inter type is decoded (prediction in wpv)
@@ -2117,6 +2304,24 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           select_sub(sel, vs >= 0, vs, vm, thr, lane);
         }
         stamp(a, mb, 4);
+        acct_add(a.acct, Acct::kCoderSearch, acct_now() - tacc);
+        if (early) {  // the group's records (and the cross-frame dependencies), then this MB's
+          tacc = acct_now();
+          if (tid == 0) {
+            if (!ready0) {
+              if (by_tag) rec_settle(a, grec, gran_ld(grec), by, mb);
+              else wait_records(a, by, bx >> 2);
+              acquire_fence(a.sys);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the acquire has completed
+          }
+          __syncthreads();
+          acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
+          tacc = acct_now();
+          if (tid < kGranulesPerMB && pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);
+          load_inter();
+          acct_add(a.acct, Acct::kCoderInter, acct_now() - tacc);
+        }
         d = make_desc(sel, px, py, thr, true, 0);
         int best_sad = sel.sad;
 
@@ -2333,8 +2538,10 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     if (kGroupSource && a.inter) group_source(a, r, g, L.inter);
     if (a.inter && a.nref >= 2) {
       helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+      const uint64_t ts = acct_now();
       if (kGroupSource) zero_mv_older(a, r, g, L.inter);
       for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is, 0);
+      acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
     }
     // level 1 of the group's window in the previous frame; deblock meanwhile
     // (a deblock chunk started here delays the search when the previous
@@ -2344,7 +2551,9 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
+      const uint64_t ts = acct_now();
       inter_task(a, r, g, 1, L.inter, L.db, st, flag, is, a.nref);  // publishes the group's nref records
+      acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2352,13 +2561,18 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     }
     if (is) is[2] = __builtin_amdgcn_s_memrealtime();
     int caught = 0;
+    const uint64_t tc = acct_now();
+    uint64_t tcdb = 0;
     for (; !kCoderDeblock;) {  // catch the deblock up with what has arrived
       int d = 0;
       if (tid == 0) d = !kCoderDeblock && kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
       if (!wg_broadcast(vflag, d)) break;
+      const uint64_t tb = acct_now();
       deblock_chunk(a, r, L.db, st, true);
+      tcdb += acct_now() - tb;
       caught++;
     }
+    acct_add(a.acct, Acct::kHelperCatchup, acct_now() - tc - tcdb);
     if (is) is[11] = ((uint64_t)caught << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - is[2]);
   }
   trace(tr, 1, 1000);
@@ -2554,23 +2768,34 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
     if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(CAIRO_PRIO_LEVEL);
     for (;;) {
       bool prev;
+      const uint64_t tq = acct_now();
       const int t = next_task(e, 0, lab, L, prev);
+      acct_add(e.acct, Acct::kHelperDequeue, acct_now() - tq);
       if (t < 0) break;
       trace(e.trace, 0, 1000000 + t);
       const int32_t o = (prev ? e.porder : e.order)[0][t];
+      const uint64_t tt = acct_now();
       row_helper(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.helper, &L.flag, e.trace);
       task_done(prev ? e.psync : e.sync);
+      acct_add(e.acct, Acct::kHelperTotal, acct_now() - tt);
+      acct_add(e.acct, Acct::kHelperTasks, 1);
       trace(e.trace, 0, 2000000 + t);
     }
   } else {
     for (;;) {
       bool prev;
+      const uint64_t tq = acct_now();
       const int t = next_task(e, 1, lab, L, prev);
+      acct_add(e.acct, Acct::kCoderDequeue, acct_now() - tq);
       if (t < 0) break;
       trace(e.trace, 0, 3000000 + t);
       const int32_t o = (prev ? e.porder : e.order)[1][t];
+      const uint64_t tt = acct_now();
       code_row<kDecode>(((FA*)(prev ? e.pfa : e.fa))[uni(o >> 16)], o & 0xFFFF, L.u.row, &L.flag, e.trace);
       task_done(prev ? e.psync : e.sync);
+      acct_add(e.acct, Acct::kCoderTotal, acct_now() - tt);
+      acct_add(e.acct, Acct::kCoderTasks, 1);
+      acct_add(e.acct, Acct::kCoderMBs, (uint64_t)e.wmb);
       trace(e.trace, 0, 4000000 + t);
     }
   }
@@ -2638,6 +2863,7 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   // 4940 / 5040)
   a.db_shift = CAIRO_DB_CHUNK ? __builtin_ctz(CAIRO_DB_CHUNK) : (e.wmb >= 200 ? 6 : e.wmb >= 100 ? 5 : 4);
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
+  a.acct = e.acct;
   {
     const int ng = (e.wmb + 3) / 4;
     a.istamps = e.stamps ? e.stamps + (size_t)kMaxBatch * stamp_frame_words(e.wmb, e.hmb) + 2 +
