@@ -499,8 +499,8 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
 #define CAIRO_WIN_DMA 1
 #endif
 typedef __attribute__((address_space(3))) void lds_void;
-__device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
-                                                int r1, int c0, int c1) {
+__device__ __forceinline__ void dma_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
+                                           int r1, int c0, int c1) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   {  // luma: rows r0 + wave, r0 + wave + 4, ...; lane = column pair
     const int c = 2 * lane, gx = ox + c;
@@ -524,10 +524,12 @@ __device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, in
                                          (lds_void*)&(pl ? w.v : w.u)[r * kWinCP], 2, 0, 0);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
-  __syncthreads();                                    // ... every wave's
-  // bias the staged region (v ^ 0x8000) in 16-byte chunks: luma 16 lanes per
-  // row (8 columns each), chroma 8 lanes per row
+}
+// Bias window rows [r0, r1) x columns [c0, c1) in LDS (v ^ 0x8000), in
+// 16-byte chunks: luma 16 lanes per row (8 columns each), chroma 8 lanes per
+// row.  All 256 threads; after every wave's DMA has landed (vmcnt, barrier).
+__device__ __forceinline__ void bias_window(Window& w, int r0, int r1, int c0, int c1) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   {
     const int k0 = c0 >> 3, k1 = c1 >> 3;  // luma chunks of the staged columns
     const int rr = lane >> 4, kk = lane & 15;
@@ -545,6 +547,13 @@ __device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, in
         *q = bias4(*q);
       }
   }
+}
+__device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
+                                                int r1, int c0, int c1) {
+  dma_window(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
+  __syncthreads();                                    // ... every wave's
+  bias_window(w, r0, r1, c0, c1);
 }
 
 __device__ __forceinline__ void stage_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
@@ -875,12 +884,15 @@ __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st);
 // index-back (back = 1: the previous frame, 2: the one before) of MB row rr
 // reaches need, running this row's ready deblock chunks meanwhile; then
 // acquire what the progress word released.  Bounded like every wait (the
-// error word ends it).
+// error word ends it).  full (LDS, optional): also whether rows rr and r+3
+// are final through full_cols (the whole search window, inter_task), from
+// the same polls -- covered by the same acquire.
 template <bool kDeblock = true>
 __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int need, DbLds& D,
-                                            DbState& st, int* flag) {
+                                            DbState& st, int* flag, int* full = nullptr, int full_cols = 0) {
   volatile int* vflag = flag;
   const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
+  const int r3 = min(r + 3, a.hmb - 1);
   uint64_t t0 = 0;
   const uint64_t ta = acct_now();
   uint64_t tdb = 0;  // accounting: time in deblock chunks run here
@@ -890,9 +902,11 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
 #if CAIRO_READY_PAIR
       // the progress poll and the deblock readiness loads in flight together
       const uint64_t pv = pp ? progress_peer(a.sys, pp + rr) : ~0ull;
+      const uint64_t p3 = pp && full ? progress_peer(a.sys, pp + r3) : ~0ull;
       const bool dbr = kDeblock && !kCoderDeblock && kHelperInterleave && deblock_pending(a, st) &&
                        deblock_chunk_ready(a, r, st);
 #else
+      const uint64_t p3 = pp && full ? progress_peer(a.sys, pp + r3) : ~0ull;
       const uint64_t pv = pp ? progress_peer(a.sys, pp + rr) : ~0ull;
       const bool dbr = pv < tagged(a.epoch - back, need) && kDeblock && !kCoderDeblock && kHelperInterleave &&
                        deblock_pending(a, st) && deblock_chunk_ready(a, r, st);
@@ -900,8 +914,13 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
       if (a.inject && r == min(1, a.hmb - 1)) {  // test hook: this wait "times out" at once
         report_timeout(a, kWaitInjected, r, need, rr | (back << 16), pv);
         d = 1;
+        if (full) *(volatile int*)full = 0;
       } else if (pv >= tagged(a.epoch - back, need)) {
         d = 1;
+        if (full) {
+          const uint64_t want = tagged(a.epoch - back, full_cols);
+          *(volatile int*)full = (pv >= want) & (p3 >= want);
+        }
       } else if (dbr) {
         d = 2;
       } else {  // nothing to do: back off
@@ -914,6 +933,7 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
           report_timeout(a, kWaitPrevProgress, r, need, rr | (back << 16), pv);
           d = 1;
         }
+        if (d && full) *(volatile int*)full = 0;
       }
     }
     d = wg_broadcast(vflag, d);
@@ -935,10 +955,18 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
 #ifndef CAIRO_DB_IN_WAIT1
 #define CAIRO_DB_IN_WAIT1 1
 #endif
+
 #ifndef CAIRO_GROUP_SOURCE
 #define CAIRO_GROUP_SOURCE 1
 #endif
 constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
+// Window DMA issued before the zero-MV loads (one round trip for both), with
+// the whole-window finality taken from the preceding helper_wait (1), or
+// staged after the zero-MV check (0).
+#ifndef CAIRO_SPEC_STAGE
+#define CAIRO_SPEC_STAGE 1
+#endif
+constexpr bool kSpecStage = CAIRO_SPEC_STAGE && CAIRO_WIN_DMA && CAIRO_GROUP_SOURCE;
 
 struct InterLds {
   Window win;
@@ -1024,8 +1052,14 @@ __device__ __forceinline__ int inter_need_cols(FA& a, int g, int level) {
 // publish = 0: the task's records stay in flight (a later task of the group
 // drains them); publish = n: drain this wave's stores and add n to the group's
 // finished count (the coder waits for nref).
+// hint >= 0: whether the reference is final over the whole window, as the
+// caller's helper_wait found (with its acquire); the task then skips its own
+// check.  staged: the caller has issued the window's DMA for this reference
+// (whole window if hint, else level 1) before the zero-MV loads, which waited
+// for it; only the bias pass remains (kSpecStage).
 __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLds& L, DbLds& D,
-                                           DbState& st, int* flag, uint64_t* is, int publish) {
+                                           DbState& st, int* flag, uint64_t* is, int publish, int hint = -1,
+                                           bool staged = false) {
   const int wave = uni(threadIdx.x >> 6);  // scalar: the acceptance replay runs on SGPRs
   const int x = 4 * g + wave;
   const bool valid = x < a.wmb;
@@ -1041,6 +1075,13 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   s.sp_idx = s.sp_amt = s.sp_en = 0;
   s.sad = s.mad = 0;
   SrcRow srow;  // biased source rows of this lane's group slot (integer steps)
+  const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
+  if (kSpecStage && hint >= 0 && off == 1) {
+    // the window in flight with the zero-MV loads below (one round trip for
+    // both); discarded if no macroblock needs the search
+    dma_window(L.win, ref, a.wa, a.ha, ox, oy, 0, hint ? kWinL : kLvl1Rows, 0, hint ? kWinLW : kLvl1Cols);
+    staged = true;
+  }
   if (valid && kGroupSource) {  // the source from the group's LDS copy
     src = src_px_lds(L, wave);
     srow = src_rows_lds(L, wave, threadIdx.x & 15);
@@ -1056,7 +1097,8 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   }
   const bool need = valid && s.mad >= thr;
   if ((threadIdx.x & 63) == 0) L.need[wave] = need;
-  if (threadIdx.x == 0) {
+  if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's window DMA has landed
+  if (hint < 0 && threadIdx.x == 0) {
     // Is the reference already final over the whole window (level 2 too)?
     // Always, in practice, for the older references (frame index-2 runs far
     // ahead): then the window is staged in one go and the steps skip the
@@ -1082,9 +1124,11 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   __syncthreads();
   if (is && off == 1) is[3] = __builtin_amdgcn_s_memrealtime();
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
-    const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
     const bool full = L.full != 0;  // workgroup-uniform
-    stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
+    if (staged)
+      bias_window(L.win, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
+    else
+      stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     __syncthreads();
     if (is && off == 1) is[4] = __builtin_amdgcn_s_memrealtime();
     bool lvl2c = full, lvl2r = full;  // workgroup-uniform
@@ -2537,22 +2581,30 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     // searches fill what used to be the wait for the previous frame.
     if (kGroupSource && a.inter) group_source(a, r, g, L.inter);
     if (a.inter && a.nref >= 2) {
-      helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+      helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag,
+                  kSpecStage ? &L.inter.full : nullptr, inter_need_cols(a, g, 2));
       const uint64_t ts = acct_now();
+      const int full2 = kSpecStage ? L.inter.full : -1;  // (written before helper_wait's barriers)
+      if (kSpecStage)  // reference 2's window in flight with the zero-MV loads of references 2..R-1
+        dma_window(L.inter.win, RECON_AT(a, 2), a.wa, a.ha, 4 * g * kMB - 32, r * kMB - 32, 0,
+                   full2 ? kWinL : kLvl1Rows, 0, full2 ? kWinLW : kLvl1Cols);
       if (kGroupSource) zero_mv_older(a, r, g, L.inter);
-      for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is, 0);
+      for (int off = 2; off <= a.nref; off++)
+        inter_task(a, r, g, off, L.inter, L.db, st, flag, is, 0, full2, kSpecStage && off == 2);
       acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
     }
     // level 1 of the group's window in the previous frame; deblock meanwhile
     // (a deblock chunk started here delays the search when the previous
     // frame's progress arrives meanwhile: CAIRO_DB_IN_WAIT1 = 0 leaves the
     // chunks to the catch-up after the group's records)
-    helper_wait<CAIRO_DB_IN_WAIT1 != 0>(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
+    helper_wait<CAIRO_DB_IN_WAIT1 != 0>(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag,
+                                        kSpecStage && a.inter ? &L.inter.full : nullptr, inter_need_cols(a, g, 2));
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
       const uint64_t ts = acct_now();
-      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is, a.nref);  // publishes the group's nref records
+      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is, a.nref,  // publishes the group's nref records
+                 kSpecStage ? L.inter.full : -1);
       acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
