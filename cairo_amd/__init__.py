@@ -272,13 +272,15 @@ class Context:
 
     ACCT_FIELDS = ("coder_tasks", "coder_total", "coder_group_wait", "coder_window", "coder_search", "coder_inter",
                    "coder_dequeue", "coder_mbs", "helper_tasks", "helper_total", "helper_wait", "helper_deblock",
-                   "helper_search", "helper_catchup", "helper_dequeue", "helper_chunks")
+                   "helper_search", "helper_catchup", "helper_dequeue", "helper_chunks",
+                   "win_bytes", "win_spec_unused_bytes", "zero_mv_bytes", "gran_poll_bytes", "rec_poll_bytes",
+                   "win_stages", "searched_tasks", "inter_tasks")
 
     def read_acct(self, reset: bool = False) -> dict:
         """Engine time accounting (set_debug(32) on a CAIRO_ACCT=1 build): 10 ns
         ticks per role and phase summed over all tasks (kernels.h Acct)."""
-        w = np.zeros(16, np.uint64)
-        _ck(self.L.cairo_ctx_read_acct(self.h, _ptr(w), 16, int(reset)), "cairo_ctx_read_acct")
+        w = np.zeros(len(self.ACCT_FIELDS), np.uint64)
+        _ck(self.L.cairo_ctx_read_acct(self.h, _ptr(w), len(w), int(reset)), "cairo_ctx_read_acct")
         return {k: int(w[i]) for i, k in enumerate(self.ACCT_FIELDS)}
 
     def timeout_info(self) -> dict | None:

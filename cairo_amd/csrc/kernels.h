@@ -112,7 +112,7 @@ enum TimeoutKind : int32_t {
 #ifndef CAIRO_ACCT
 #define CAIRO_ACCT 0
 #endif
-constexpr int kAcctShards = 64, kAcctWords = 16;
+constexpr int kAcctShards = 64, kAcctWords = 24;
 struct Acct {
   // row coders
   static constexpr int kCoderTasks = 0, kCoderTotal = 1, kCoderGroupWait = 2, kCoderWindow = 3, kCoderSearch = 4,
@@ -120,6 +120,9 @@ struct Acct {
   // row helpers
   static constexpr int kHelperTasks = 8, kHelperTotal = 9, kHelperWait = 10, kHelperDeblock = 11, kHelperSearch = 12,
                        kHelperCatchup = 13, kHelperDequeue = 14, kHelperChunks = 15;
+  // traffic of the staging and the polls (bytes requested, nominal)
+  static constexpr int kWinBytes = 16, kWinSpecUnused = 17, kZeroMvBytes = 18, kGranPollBytes = 19,
+                       kRecPollBytes = 20, kWinStages = 21, kSearchedTasks = 22, kInterTasks = 23;
 };
 
 // Frames per engine launch.

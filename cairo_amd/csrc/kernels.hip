@@ -286,6 +286,12 @@ __device__ __forceinline__ uint32_t rec_settle(FA& a, const uint64_t* p, uint64_
   for (;;) {
     __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
     g = gran_ld(p);
+    if (CAIRO_ACCT && a.acct) {
+      const uint64_t act = __ballot(1);
+      if ((int)(threadIdx.x & 63) == __ffsll((long long)act) - 1)
+        __hip_atomic_fetch_add(&a.acct[(blockIdx.x & (kAcctShards - 1)) * kAcctWords + Acct::kRecPollBytes],
+                               8ull * __popcll(act), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if ((uint32_t)(g >> 32) == a.epoch) break;
     if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
@@ -305,6 +311,12 @@ __device__ __forceinline__ uint32_t gran_settle(FA& a, const uint64_t* p, uint64
   for (;;) {
     __builtin_amdgcn_s_sleep(CAIRO_GRAN_SLEEP);
     g = gran_ld(p);
+    if (CAIRO_ACCT && a.acct) {  // this wave's re-poll: 8 bytes per active lane
+      const uint64_t act = __ballot(1);
+      if ((int)(threadIdx.x & 63) == __ffsll((long long)act) - 1)
+        __hip_atomic_fetch_add(&a.acct[(blockIdx.x & (kAcctShards - 1)) * kAcctWords + Acct::kGranPollBytes],
+                               8ull * __popcll(act), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if ((uint32_t)(g >> 32) == a.epoch) break;
     if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
@@ -556,6 +568,10 @@ __device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, in
   bias_window(w, r0, r1, c0, c1);
 }
 
+__device__ __forceinline__ void acct_window(uint64_t* acct, int r0, int r1, int c0, int c1) {
+  acct_add(acct, Acct::kWinBytes, (uint64_t)(r1 - r0) * (c1 - c0) * 3);  // luma + 2 quarter chroma planes, int16
+  acct_add(acct, Acct::kWinStages, 1);
+}
 __device__ __forceinline__ void stage_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
                                              int r1, int c0, int c1) {
   if (CAIRO_WIN_DMA)
@@ -1027,6 +1043,7 @@ __device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int wave, int 
 // index-2's level-1 window (which covers the zero-MV block).
 __device__ __forceinline__ void zero_mv_older(FA& a, int r, int g, InterLds& L) {
   const int wave = threadIdx.x >> 6, x = 4 * g + wave;
+  acct_add(a.acct, Acct::kZeroMvBytes, 768ull * (a.nref - 1) * (uint64_t)min(4, a.wmb - 4 * g));
   if (x >= a.wmb) return;
   const int px = x * kMB, py = r * kMB;
   const Px6 src = src_px_lds(L, wave);
@@ -1123,8 +1140,14 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   }
   __syncthreads();
   if (is && off == 1) is[3] = __builtin_amdgcn_s_memrealtime();
+  acct_add(a.acct, Acct::kInterTasks, 1);
+  acct_add(a.acct, Acct::kZeroMvBytes, (off == 1 ? 768ull : 0ull) * (uint64_t)min(4, a.wmb - 4 * g));
+  if (CAIRO_ACCT && !(L.need[0] | L.need[1] | L.need[2] | L.need[3]) && staged)
+    acct_add(a.acct, Acct::kWinSpecUnused, (uint64_t)(L.full ? kWinL * kWinLW : kLvl1Rows * kLvl1Cols) * 3);
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
     const bool full = L.full != 0;  // workgroup-uniform
+    acct_add(a.acct, Acct::kSearchedTasks, 1);
+    acct_window(a.acct, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     if (staged)
       bias_window(L.win, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     else
@@ -1159,6 +1182,8 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
                              D, st, flag);
           if (m & 2) stage_window(L.win, ref, a.wa, a.ha, ox, oy, kLvl1Rows, kWinL, 0, kWinLW);
           if (!lvl2c) stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, kLvl1Rows, kLvl1Cols, kWinLW);
+          if (m & 2) acct_window(a.acct, kLvl1Rows, kWinL, 0, kWinLW);
+          if (!lvl2c) acct_window(a.acct, 0, kLvl1Rows, kLvl1Cols, kWinLW);
           __syncthreads();
           if (is) is[6] = __builtin_amdgcn_s_memrealtime(), is[7] += (m & 2) ? 0x10000 : 1;
           lvl2c = true;

@@ -162,8 +162,9 @@ CAIRO_API int cairo_ctx_read_trace(cairo_ctx *ctx, int32_t *out, int n);
 CAIRO_API int cairo_ctx_timeout_info(cairo_ctx *ctx, int32_t *out, int n);
 /* Debug: flags & 32 turns on the engine's time accounting, which a library
  * built with CAIRO_ACCT=1 (tools/build_variant.sh) fills: per role and phase,
- * the 10 ns ticks summed over every task since the last reset (16 words,
- * kernels.h Acct; zeros from a regular build).  Synchronous; reset = 1 zeroes
+ * the 10 ns ticks summed over every task since the last reset, then bytes
+ * requested by the window staging and the polls (24 words, kernels.h Acct;
+ * zeros from a regular build).  Synchronous; reset = 1 zeroes
  * the counters after reading them. */
 CAIRO_API int cairo_ctx_read_acct(cairo_ctx *ctx, uint64_t *out, int n, int reset);
 CAIRO_API int cairo_ctx_read_predeblock(cairo_ctx *ctx, int16_t *y, int16_t *u, int16_t *v);

@@ -64,8 +64,14 @@ def main():
     helper["rest"] = round(helper["total"] - sum(helper[k] for k in ("wait", "deblock", "search", "catchup")), 3)
     helper["dequeue_per_task"] = round(us(c["helper_dequeue"]) / max(c["helper_tasks"], 1), 2)
     helper["chunks_per_group"] = round(c["helper_chunks"] / groups, 3)
+    mb = 1e6
+    traffic = {k: round(c[k] / timed / mb, 2) for k in
+               ("win_bytes", "win_spec_unused_bytes", "zero_mv_bytes", "gran_poll_bytes", "rec_poll_bytes")}
+    traffic["unit"] = "MB per frame (requested)"
+    traffic["searched_task_frac"] = round(c["searched_tasks"] / max(c["inter_tasks"], 1), 3)
+    traffic["win_stages_per_frame"] = round(c["win_stages"] / timed, 1)
     out = {"config": a.config, "timed_frames": timed, "mpix_s": round(w * h * timed / el / 1e6, 1),
-           "coder_us_per_mb": coder, "helper_us_per_group": helper, "raw": c}
+           "coder_us_per_mb": coder, "helper_us_per_group": helper, "traffic": traffic, "raw": c}
     print(json.dumps(out))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
