@@ -329,3 +329,36 @@ def test_many_launches_queued(orc, cairo):
         ctx.close()
     finally:
         hip.hipFree(dev)
+
+
+def test_host_rgb_release_without_wait(orc, cairo):
+    """A caller may release a ticket without waiting for it (cairo_ctx_release
+    needs no wait).  Host RGB frames are uploaded at submit into their staging
+    slot's buffer, so a later frame's upload into the same slot must wait for
+    the launch that converts the earlier frame (backend.hip rgb_read), or the
+    earlier frame is encoded from the later image.  4 staging slots, 2 frames
+    per launch, every ticket but the last released unwaited: the final ring
+    slots and the last frame's outputs equal the oracle's."""
+    w, h, ring, q, n = 352, 288, 4, 16, 14
+    ctx = cairo.Context(w, h, ring, stages=4)
+    ctx.set_batch(2)
+    e = orc.OracleEncoder(ring)
+    e.set_quality(q)
+    tk = None
+    for t in range(n):
+        rgb = orc.make_frame(w, h, t)
+        e.encode(rgb)
+        tk = ctx.submit(rgb, t, t > 0, q)
+        if t < n - 1:
+            ctx.release(tk)
+    out = ctx.wait(tk)
+    _table_equal(out.table, e.block_table(), "last frame")
+    np.testing.assert_array_equal(out.coef_y, e.planes(1)[0])
+    ctx.release(tk)
+    ctx.sync()
+    for k in range(ring):
+        gy, gu, gv = ctx.read_planes(2 + k)
+        np.testing.assert_array_equal(gy, e.planes(2 + k)[0], err_msg=f"slot {k} Y")
+        np.testing.assert_array_equal(gu, e.planes(2 + k)[1], err_msg=f"slot {k} U")
+        np.testing.assert_array_equal(gv, e.planes(2 + k)[2], err_msg=f"slot {k} V")
+    ctx.close()
