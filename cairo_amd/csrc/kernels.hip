@@ -1517,6 +1517,11 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 constexpr int kDbChunk = 64;  // the widest chunk: luma columns (tile width, info table, arrays)
 constexpr int kDbMBs = kDbChunk / 16;
 __device__ __forceinline__ int db_chunks(const FA& a) { return (a.wa + (1 << a.db_shift) - 1) >> a.db_shift; }
+// The deblock's 4 rows above loaded all at once (1: one round trip) or one
+// load per pass of the lanes (0: the round-3 form, a round trip per pass).
+#ifndef CAIRO_ABOVE_BATCH
+#define CAIRO_ABOVE_BATCH 1
+#endif
 // The filters of a 64-column chunk over all four waves (1) or in wave 0 (0).
 #ifndef CAIRO_DB_SPREAD
 #define CAIRO_DB_SPREAD 1
@@ -1669,7 +1674,18 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           // index space: a whole chunk's dwords per row (luma 2^(s-1), chroma
           // 2^(s-2)), so that row and column are shifts
           const int s1 = a.db_shift - 1, s2 = a.db_shift - 2, nall = 8 << s1;
-          for (int i = t3 - 2 * nmb; i < nall; i += 64 - 2 * nmb) {
+          // every load of this lane issued before the first LDS store: one
+          // fabric round trip, not one per load (nall <= 256 dwords over >= 56
+          // lanes: at most kAbove each)
+          constexpr int kAbove = CAIRO_ABOVE_BATCH ? (8 << (6 - 1)) / (64 - 2 * kDbMBs) + 1 : 1;
+          uint32_t v[kAbove];
+          int16_t* dst[kAbove];
+          for (int i0 = t3 - 2 * nmb; i0 < nall; i0 += kAbove * (64 - 2 * nmb)) {  // one pass when batched
+#pragma unroll
+          for (int u = 0; u < kAbove; u++) {
+            const int i = i0 + u * (64 - 2 * nmb);
+            dst[u] = nullptr;
+            if (i >= nall) continue;
             int pl, row, col;
             const int16_t* g;
             if (i < (4 << s1)) {
@@ -1683,11 +1699,16 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
               pl = 1 + pj, row = jj >> s2, col = (c0 >> 1) + 2 * d;
               g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
             }
-            const uint32_t d = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int16_t* p = db_px(D, pl, row, col);
-            p[0] = (int16_t)(d & 0xFFFF);
-            p[1] = (int16_t)(d >> 16);
+            v[u] = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)g, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            dst[u] = db_px(D, pl, row, col);
+          }
+#pragma unroll
+          for (int u = 0; u < kAbove; u++)
+            if (dst[u]) {
+              dst[u][0] = (int16_t)(v[u] & 0xFFFF);
+              dst[u][1] = (int16_t)(v[u] >> 16);
+            }
           }
         }
       }
