@@ -2524,12 +2524,16 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       } else {  // copy: output_cache keeps this macroblock's previous coefficients
         d.q_index = 0;
         d.variance = 0;
-        if (!kDecode) _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
-          const int e = (wave + 4 * bi) * 64 + lane;
-          int pl, ex, ey;
-          elem_coords(e, px, py, pl, ex, ey);
-          const size_t o = (size_t)ey * (pl ? cw : a.wa) + ex;
-          coef_store_pair(a, e, px, py, pick(planes(a.coef_prev), pl)[o]);
+        if (!kDecode) {
+          int cp[2] = {0, 0};  // both loads issued before the first store (which may alias them)
+          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+            const int e = (wave + 4 * bi) * 64 + lane;
+            int pl, ex, ey;
+            elem_coords(e, px, py, pl, ex, ey);
+            cp[bi] = pick(planes(a.coef_prev), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+          }
+          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
+            coef_store_pair(a, (wave + 4 * bi) * 64 + lane, px, py, cp[bi]);
         }
       }
       stamp(a, mb, 7);
