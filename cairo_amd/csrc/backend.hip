@@ -656,11 +656,16 @@ int flush(cairo_ctx* c) {
     CK(launch_precode(fa, (int)c->mbs, pst));
   }
   if (!c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
-  if (c->ps_own && (c->outputs & CAIRO_OUT_FEED)) {
-    CK(hipEventRecord(c->pre_done[area], c->ps));
-    CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
-  } else {
-    CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
+  // the copy stream carries D2H copies only with the coefficient planes; in
+  // feed-only mode it carries the host-RGB uploads (submit), which must not
+  // queue behind the launches in flight
+  if (c->outputs & CAIRO_OUT_COEF) {
+    if (c->ps_own && (c->outputs & CAIRO_OUT_FEED)) {
+      CK(hipEventRecord(c->pre_done[area], c->ps));
+      CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
+    } else {
+      CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
+    }
   }
   // outputs for the host entropy stage: with the feed, the precode's last
   // kernel (k_feed_copy) has written each frame's feed, block table and
