@@ -501,8 +501,8 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
 // load of the window is in flight at once -- one fabric round trip instead of
 // one per kWinUnroll loads), then an in-LDS pass that biases the staged
 // region.  One wave instruction stages one window row: luma 64 lanes x 4 B
-// (128 columns, pitch kWinLP), chroma 64 lanes x 2 B (64 columns, pitch
-// kWinCP): an LDS-DMA writes wave-uniform base + lane x size, so each row's
+// (128 columns, pitch kWinLP), chroma 32 lanes x 4 B (64 columns, pitch
+// kWinCP): an LDS-DMA writes wave-uniform base + lane x 4, so each row's
 // padding stays outside.  Rows outside the frame are skipped; lanes whose
 // columns fall outside [c0, c1) or the frame are masked off.  All 256 threads
 // participate; ends with the bias pass's writes issued (the caller's barrier
@@ -524,16 +524,18 @@ __device__ __forceinline__ void dma_window(Window& w, const PlaneSet& p, int wa,
         __builtin_amdgcn_global_load_lds((const void*)&p.y[(size_t)gy * wa + gx], (lds_void*)&w.y[r * kWinLP], 4, 0, 0);
     }
   }
-  {  // chroma: U rows then V rows, [r0/2, r1/2); lane = column
+  {  // chroma: U rows then V rows, [r0/2, r1/2); lanes 0..31 = column pairs
+    // (an LDS-DMA writes lane x 4 bytes whatever the load size, so a 64-column
+    // chroma row is 32 dword lanes; the upper half-wave idles)
     const int cr0 = r0 >> 1, cr1 = r1 >> 1, ncr = cr1 - cr0;
-    const int cw = wa >> 1, ch = ha >> 1, cx = lane, gx = (ox >> 1) + cx;
-    const bool col_ok = 2 * cx >= c0 && 2 * cx < c1 && gx >= 0 && gx < cw;
+    const int cw = wa >> 1, ch = ha >> 1, cx = 2 * lane, gx = (ox >> 1) + cx;
+    const bool col_ok = lane < 32 && 2 * cx >= c0 && 2 * cx < c1 && gx >= 0 && gx < cw;
     for (int k = wave; k < 2 * ncr; k += 4) {
       const int pl = k >= ncr, r = cr0 + k - (pl ? ncr : 0), gy = (oy >> 1) + r;
       if (gy < 0 || gy >= ch) continue;
       if (col_ok)
         __builtin_amdgcn_global_load_lds((const void*)&pick(p, 1 + pl)[(size_t)gy * cw + gx],
-                                         (lds_void*)&(pl ? w.v : w.u)[r * kWinCP], 2, 0, 0);
+                                         (lds_void*)&(pl ? w.v : w.u)[r * kWinCP], 4, 0, 0);
     }
   }
 }
