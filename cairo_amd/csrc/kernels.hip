@@ -508,12 +508,41 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
 // participate; ends with the bias pass's writes issued (the caller's barrier
 // publishes them).
 #ifndef CAIRO_WIN_DMA
-#define CAIRO_WIN_DMA 1
+#define CAIRO_WIN_DMA 0
 #endif
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void dma_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
                                            int r1, int c0, int c1) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (CAIRO_WIN_DMA == 2) {
+    // 16-byte lanes: the window's rows are numbered as 16-byte chunks over the
+    // PADDED pitch (17 per luma row, 9 per chroma row), so one wave
+    // instruction fills 64 consecutive chunks (~3.8 luma rows) and the lanes
+    // that land in a row's pad, outside [c0, c1) or outside the frame are
+    // masked off: as many wave instructions as the register staging, every one
+    // in flight at once.
+    constexpr int kLC = kWinLP / 8, kCC = kWinCP / 8;
+    static_assert(kWinLP % 8 == 0 && kWinCP % 8 == 0, "16-byte chunked pitches");
+    const int k0 = r0 * kLC, k1 = r1 * kLC;
+    for (int kb = k0 + 64 * wave; kb < k1; kb += 256) {
+      const int k = kb + lane, r = k / kLC, cc = k - r * kLC, c = cc << 3;
+      const int gy = oy + r, gx = ox + c;
+      if (k < k1 && cc < (kWinLW >> 3) && c >= c0 && c < c1 && gy >= 0 && gy < ha && gx >= 0 && gx < wa)
+        __builtin_amdgcn_global_load_lds((const void*)&p.y[(size_t)gy * wa + gx], (lds_void*)&w.y[kb << 3], 16, 0, 0);
+    }
+    const int cr0 = r0 >> 1, cr1 = r1 >> 1, ck0 = cr0 * kCC, ck1 = cr1 * kCC;
+    const int ni = (ck1 - ck0 + 63) >> 6;  // instructions per chroma plane
+    const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
+    for (int i = wave; i < 2 * ni; i += 4) {
+      const int pl = i >= ni, kb = ck0 + ((i - (pl ? ni : 0)) << 6);
+      const int k = kb + lane, r = k / kCC, cc = k - r * kCC, c = cc << 3;
+      const int gy = coy + r, gx = cox + c;
+      if (k < ck1 && cc < 8 && 2 * c >= c0 && 2 * c < c1 && gy >= 0 && gy < ch && gx >= 0 && gx < cw)
+        __builtin_amdgcn_global_load_lds((const void*)&pick(p, 1 + pl)[(size_t)gy * cw + gx],
+                                         (lds_void*)&(pl ? w.v : w.u)[kb << 3], 16, 0, 0);
+    }
+    return;
+  }
   {  // luma: rows r0 + wave, r0 + wave + 4, ...; lane = column pair
     const int c = 2 * lane, gx = ox + c;
     const bool col_ok = c >= c0 && c < c1 && gx >= 0 && gx < wa;
@@ -984,7 +1013,7 @@ constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
 #ifndef CAIRO_SPEC_STAGE
 #define CAIRO_SPEC_STAGE 1
 #endif
-constexpr bool kSpecStage = CAIRO_SPEC_STAGE && CAIRO_WIN_DMA && CAIRO_GROUP_SOURCE;
+constexpr bool kSpecStage = CAIRO_SPEC_STAGE && CAIRO_WIN_DMA != 0 && CAIRO_GROUP_SOURCE;
 
 struct InterLds {
   Window win;

@@ -6,6 +6,9 @@
 set -e
 C=${1:-720p}; N=${2:-2}; shift 2 || true
 mkdir -p gpurun_out
+# the in-tree library is put back however the runs end
+cp cairo_amd/_lib/libcairo_amd.so gpurun_out/.ab_saved.so
+trap 'cp gpurun_out/.ab_saved.so cairo_amd/_lib/libcairo_amd.so' EXIT
 for i in $(seq 1 $N); do
   for v in $(cd scratch/ab && ls *.so | sed 's/\.so$//'); do
     cp scratch/ab/$v.so cairo_amd/_lib/libcairo_amd.so
