@@ -508,7 +508,7 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
 // participate; ends with the bias pass's writes issued (the caller's barrier
 // publishes them).
 #ifndef CAIRO_WIN_DMA
-#define CAIRO_WIN_DMA 0
+#define CAIRO_WIN_DMA 2
 #endif
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void dma_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
@@ -1011,7 +1011,7 @@ constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
 // the whole-window finality taken from the preceding helper_wait (1), or
 // staged after the zero-MV check (0).
 #ifndef CAIRO_SPEC_STAGE
-#define CAIRO_SPEC_STAGE 1
+#define CAIRO_SPEC_STAGE 0
 #endif
 constexpr bool kSpecStage = CAIRO_SPEC_STAGE && CAIRO_WIN_DMA != 0 && CAIRO_GROUP_SOURCE;
 

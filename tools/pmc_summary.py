@@ -5,6 +5,7 @@ Inputs (gpurun_out/, written by the rocprofv3 commands in DESIGN.md §Measuremen
   prof_fetch/run_counter_collection.csv --pmc FETCH_SIZE  (own pass)
   prof_write/run_counter_collection.csv --pmc WRITE_SIZE  (own pass)
   prof_sq/run_counter_collection.csv    --pmc SQ_* + GRBM_GUI_ACTIVE (wave states, optional)
+  prof_hit/run_counter_collection.csv   --pmc TCC_HIT/MISS/READ/WRITE_sum (L2 hit rate, optional)
 
 Outputs:
   profiles/<round>_<config>_kernel_stats.csv  (copy of the stats summary)
@@ -183,6 +184,20 @@ def main():
             if "TCC_EA0_RDREQ_DRAM_sum" in med and "TCC_EA0_RDREQ_sum" in med:
                 res["engine_read_requests_dram_share"] = round(med["TCC_EA0_RDREQ_DRAM_sum"] /
                                                                max(med["TCC_EA0_RDREQ_sum"], 1), 4)
+    # L2 hits / misses (one pass): how much of the requested traffic the XCD L2s absorb
+    hp = os.path.join(a.src, "prof_hit", "run_counter_collection.csv")
+    if os.path.exists(hp):
+        med = {}
+        for cn in ("TCC_HIT_sum", "TCC_MISS_sum", "TCC_READ_sum", "TCC_WRITE_sum"):
+            v = per_kernel(hp, cn).get("engine")
+            if v:
+                med[cn] = statistics.median(v)
+        if med:
+            hit, miss = med.get("TCC_HIT_sum", 0), med.get("TCC_MISS_sum", 0)
+            res["engine_l2"] = {"median_per_dispatch": med,
+                                "hit_rate": round(hit / max(hit + miss, 1), 4),
+                                "reads_per_frame": int(med.get("TCC_READ_sum", 0) / a.batch),
+                                "writes_per_frame": int(med.get("TCC_WRITE_sum", 0) / a.batch)}
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws

@@ -19,4 +19,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT
 # granule loads), so the traffic needs no blanket FETCH_SIZE correction
 timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RD_UNCACHED_32B_sum --output-format csv -d $OUT/prof_rdsize -o run -- python3 bench.py $ARGS > $OUT/prof_rdsize.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/prof_req -o run -- python3 bench.py $ARGS > $OUT/prof_req.log 2>&1
+# L2 (TCC) hits and misses of the reads and writes the CUs send it: the hit
+# rate says how much of the requested window / poll traffic the XCD L2s absorb
+timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_READ_sum TCC_WRITE_sum --output-format csv -d $OUT/prof_hit -o run -- python3 bench.py $ARGS > $OUT/prof_hit.log 2>&1
 echo "profiled $R $C: now run python tools/pmc_summary.py --round $R --config $C --src gpurun_out/prof_$C locally"
