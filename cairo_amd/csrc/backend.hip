@@ -184,6 +184,7 @@ struct cairo_ctx {
   int inject = 0;             // test hook (cairo_ctx_set_debug 16): EngineArgs::inject
   int32_t* order = nullptr;  // [kMaxBatch][kMaxBatch * hmb]: pool task order per batch size
   FrameArgs* fdesc_host = nullptr;  // pinned [kLaunchSlots][kMaxBatch]: per-frame views per launch
+  FrameArgs* fdesc_host_dev = nullptr;  // its device-visible address (read by the convert kernel)
   FrameArgs* fdesc = nullptr;       // device copy
   int fdesc_next = 0;
   // the H2D copy of each fdesc_host slot: a slot is rewritten only after its
@@ -585,17 +586,29 @@ int flush(cairo_ctx* c) {
       CK(hipMemcpyAsync(coef_base(c, f.slot), f.host_coef, c->plane_elems * 2, hipMemcpyHostToDevice, st));
     }
   }
-  CK(hipMemcpyAsync(fd, fh, sizeof(FrameArgs) * e.nframes, hipMemcpyHostToDevice, st));
-  CK(hipEventRecord(c->fdesc_done[fslot], st));
-  c->fdesc_used[fslot] = true;
-  CK(hipMemsetAsync(e.sync, 0, c->sync_words * sizeof(int32_t), st));
+  // the frame views and the zeroed sync area are written by the convert
+  // kernel below (ConvertArgs), not by runtime copy / fill kernels
+  ConvertArgs ca{};
+  ca.w = e.w, ca.h = e.h, ca.wa = e.wa, ca.nframes = e.nframes;
+  for (int i = 0; i < e.nframes; i++) {
+    ca.rgb[i] = fh[i].decode ? nullptr : fh[i].rgb;
+    ca.in[i] = fh[i].in;
+  }
+  static_assert(sizeof(FrameArgs) % sizeof(uint4) == 0, "frame views copied in 16-byte chunks");
+  ca.fa_host = (const uint4*)(c->fdesc_host_dev + (size_t)fslot * kMaxBatch);
+  ca.fa_dev = (uint4*)fd;
+  ca.fa_chunks = (int)(sizeof(FrameArgs) * e.nframes / sizeof(uint4));
+  ca.sync = e.sync;
+  ca.sync_words = (int)c->sync_words;
   if (c->stamps) {  // engine entry (min) / exit (max) words
     static const uint64_t init[2] = {~0ull, 0};
     CK(hipMemcpyAsync(c->stamps + kMaxBatch * stamp_frame_words((int)c->wmb, (int)c->hmb), init, sizeof(init),
                       hipMemcpyHostToDevice, st));
   }
   if (tb) CK(hipEventRecord(tb->ev[0], st));
-  CK(launch_convert_batch(e, st));
+  CK(launch_convert_batch(ca, st));
+  CK(hipEventRecord(c->fdesc_done[fslot], st));  // fh has been read
+  c->fdesc_used[fslot] = true;
   for (int i = 0; i < e.nframes; i++) {  // staged host RGB converted: the buffer may be refilled
     const FrameDesc& f = c->pend[i];
     Stage& s = c->st[f.slot];
@@ -854,7 +867,8 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipMalloc(&c->sticky, TimeoutInfo::kWords * sizeof(int32_t)));
   TRY(hipMemset(c->sticky, 0, TimeoutInfo::kWords * sizeof(int32_t)));
   {  // (frame, row) task order of the engine pools, for every batch size
-    TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch, hipHostMallocDefault));
+    TRY(hipHostMalloc(&c->fdesc_host, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch, hipHostMallocMapped));
+    TRY(hipHostGetDevicePointer((void**)&c->fdesc_host_dev, c->fdesc_host, 0));
     TRY(hipMalloc(&c->fdesc, sizeof(FrameArgs) * kLaunchSlots * kMaxBatch));
     TRY(hipMalloc(&c->order, OrderBlock::words((int)c->hmb) * sizeof(int32_t)));
     r = upload_orders(c, kOrderSlope);

@@ -328,8 +328,25 @@ __host__ __device__ inline int task_label(int frame, int row, int hmb) {
   return ((row >> (CAIRO_BAND_SHIFT < 0 ? 0 : CAIRO_BAND_SHIFT)) + frame * CAIRO_BAND_ROT) & (kLabels - 1);
 }
 
-// RGB -> YUV of every frame of the batch into its slot's source planes.
-hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s);
+// A launch's preparation, done by the convert kernel that precedes its
+// engine on the stream (no runtime copy or fill kernels, which would compete
+// with the co-resident engine launch for workgroup slots): RGB -> YUV of every
+// frame (pointers here, so the convert reads nothing from the frame views),
+// the frame views from mapped pinned host memory to the device, and the zeroed
+// sync area.
+struct ConvertArgs {
+  int w, h, wa, nframes;
+  const uint8_t* rgb[kMaxBatch];  // nullptr: nothing to convert (a decoded frame)
+  PlaneSet in[kMaxBatch];
+  const uint4* fa_host;  // [fa_chunks] the frame views (device-visible pinned host memory)
+  uint4* fa_dev;
+  int fa_chunks;
+  int32_t* sync;  // [sync_words], zeroed
+  int sync_words;
+};
+// RGB -> YUV of every frame of the batch into its slot's source planes, plus
+// the views and sync area above (grid slice z = nframes).
+hipError_t launch_convert_batch(const ConvertArgs& c, hipStream_t s);
 // The pipelined encode engine: inter search, macroblock rows (intra search,
 // classify, transform, quantize, reconstruct) and in-loop deblock.
 hipError_t launch_engine(const EngineArgs& e, hipStream_t s);

@@ -340,16 +340,24 @@ __device__ __forceinline__ int dequeue(int32_t* ticket, int* lds_slot) {
 // K0: RGB888 -> YUV 4:2:0 int16 (convert.cpp:11-14, 30-73, 95-160)
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_convert_batch(EngineArgs e) {
-  const FrameArgs& f = e.fa[blockIdx.z];
+__global__ __launch_bounds__(256) void k_convert_batch(ConvertArgs e) {
+  if ((int)blockIdx.z == e.nframes) {
+    // the launch's frame views (mapped host memory -> device) and zeroed sync
+    // area, spread over the slice's blocks
+    const int nb = gridDim.x * gridDim.y, t = (blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+    for (int k = t; k < e.fa_chunks; k += nb * 256) e.fa_dev[k] = e.fa_host[k];
+    for (int k = t; k < e.sync_words; k += nb * 256) e.sync[k] = 0;
+    return;
+  }
+  const uint8_t* rgb = e.rgb[blockIdx.z];
   const int qx = blockIdx.x * 256 + threadIdx.x;  // quad column
   const int qy = blockIdx.y;                      // quad row
-  if (qx >= (e.w >> 1) || f.decode) return;
-  const PlaneSet in = f.in;
+  if (qx >= (e.w >> 1) || !rgb) return;
+  const PlaneSet in = e.in[blockIdx.z];
   int su = 0, sv = 0;
 #pragma unroll
   for (int dy = 0; dy < 2; dy++) {
-    const uint8_t* p = f.rgb + ((size_t)(2 * qy + dy) * e.w + 2 * qx) * 3;
+    const uint8_t* p = rgb + ((size_t)(2 * qy + dy) * e.w + 2 * qx) * 3;
     int16_t* y = in.y + (size_t)(2 * qy + dy) * e.wa + 2 * qx;
 #pragma unroll
     for (int dx = 0; dx < 2; dx++) {
@@ -363,8 +371,8 @@ __global__ __launch_bounds__(256) void k_convert_batch(EngineArgs e) {
   in.v[(size_t)qy * (e.wa >> 1) + qx] = (int16_t)((sv + 2) >> 2);
 }
 
-hipError_t launch_convert_batch(const EngineArgs& e, hipStream_t s) {
-  dim3 grid((e.w / 2 + 255) / 256, e.h / 2, e.nframes);
+hipError_t launch_convert_batch(const ConvertArgs& e, hipStream_t s) {
+  dim3 grid((e.w / 2 + 255) / 256, e.h / 2, e.nframes + 1);
   hipLaunchKernelGGL(k_convert_batch, grid, dim3(256), 0, s, e);
   return hipGetLastError();
 }
@@ -1044,6 +1052,22 @@ __device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L) {
     gsrc = pick(in, 1 + (k >> 3)) + (size_t)((py >> 1) + (k & 7)) * (a.wa >> 1) + (px >> 1);
   }
   *(uint4*)&L.src[wave][8 * lane] = *(const uint4*)gsrc;
+}
+
+// Macroblock (x, r)'s source into dst (group_source's layout) by ONE LDS-DMA
+// wave instruction of wave 0, lanes 0..47 (16 bytes each; an LDS-DMA writes
+// dst + lane x 16).  The source planes do not change during a launch.  Lands
+// behind wave 0's next vmcnt wait; readable by every wave after the barrier
+// that follows it.
+__device__ __forceinline__ void src_dma(FA& a, int x, int r, int16_t* dst) {
+  const int lane = threadIdx.x;
+  if (lane >= 48) return;
+  const PlaneSet in = planes(a.in);
+  const int px = x * kMB, py = r * kMB;
+  const int16_t* gsrc = lane < 32 ? in.y + (size_t)(py + (lane >> 1)) * a.wa + px + 8 * (lane & 1)
+                                  : pick(in, 1 + ((lane - 32) >> 3)) +
+                                        (size_t)((py >> 1) + (lane & 7)) * (a.wa >> 1) + (px >> 1);
+  __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)dst, 16, 0, 0);
 }
 
 // This lane's Px6 slice (px_from_planes layout) and its SrcRow (load_src_rows
@@ -1888,8 +1912,22 @@ struct alignas(16) RowWindow {
   int16_t v[40 * kCwCP];
 };
 
+// The row coder's source macroblocks through LDS: wave 0 stages macroblock
+// bx+1's source (src_dma) while bx is coded, so neither the source rows at a
+// macroblock's start nor the residual's source elements after its search
+// cost a fabric round trip.  1: issued at the macroblock's start, with the
+// fresh granule load (an LDS-DMA in flight makes the compiler drain vmcnt at
+// the next barrier or global-load use: hipcc, ROCm 7.2), 2: just before the
+// macroblock's final drain.  0: both read from the planes.
+#ifndef CAIRO_SRC_DMA
+#define CAIRO_SRC_DMA 1
+#endif
+constexpr int kSrcDma = CAIRO_SRC_DMA;
+constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+
 struct alignas(16) RowLds {
   RowWindow win;
+  alignas(16) int16_t src[2][384];  // source macroblocks bx, bx+1 (by bx & 1), group_source layout
   int16_t bufA[kMBElems], bufB[kMBElems];  // per-block transform scratch, block-major
   int32_t cand[2][16][2];                  // double-buffered candidate (sad, mad)
   int32_t red[12];
@@ -2200,6 +2238,11 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
 #endif
   {
     const int py = by * kMB, oy = py - 48;
+    if (kSrcDma && !kDecode) {  // macroblock 0's source; later ones are staged a macroblock ahead
+      src_dma(a, 0, by, L.src[0]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     for (int bx = 0; bx < a.wmb; bx++) {
       const int px = bx * kMB, mb = by * a.wmb + bx;
       trace(tr, 1, bx);
@@ -2210,6 +2253,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // load is issued before the group-start wait below, so that a granule
       // already there costs no round trip after it (the tag is the flag: a
       // 64-bit load needs no acquire).
+      // macroblock bx+1's source into LDS, in flight with the fresh granule
+      // load below, whose wait covers it (the buffer was last read in bx-1)
+      if (kSrcDma == 1 && !kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
       const bool fresh_col = by > 0 && bx != 0 && bx + 2 < a.wmb && tid < kGranulesPerMB;
       const uint64_t* fresh_gp = fresh_col ? gran_at(a, bx + 2, by - 1, tid) : nullptr;
       const uint64_t fresh_g = (kEarlyGran && fresh_col) ? gran_ld(fresh_gp) : 0;
@@ -2273,13 +2319,26 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         }
       }
       acct_add(a.acct, Acct::kCoderWindow, acct_now() - tacc);
+      // the source DMA has landed (free where the granule wait above covered
+      // it): a wait the compiler sees, so it knows no LDS-DMA is in flight and
+      // the barrier before the search does not drain the loads issued below
+      if (kSrcDma == 1 && !kDecode) __builtin_amdgcn_s_waitcnt(kWaitVm0);
       if (early && tid == 0) {
         ready0 = by_tag ? (uint32_t)(rd0 >> 32) == a.epoch : (int)rd0 >= a.nref;
         if (ready0) acquire_fence(a.sys);  // completes during the search; waited for after it
       }
       // source rows of this lane's group slot
       SrcRow s;  // biased u16 pairs (the encoder's source; unused when decoding)
-      if (!kDecode) {
+      if (!kDecode && kSrcDma) {
+        // staged in LDS during macroblock bx-1 (landed behind its final drain
+        // and barrier; at bx == 0 behind the row start's)
+        const uint32_t* m = (const uint32_t*)L.src[bx & 1];
+#pragma unroll
+        for (int k = 0; k < 8; k++) s.y[k] = m[gi * 8 + k] ^ 0x80008000u;
+        const int co = (gi >> 1) * 4 + (gi & 1) * 2;
+        s.u[0] = m[128 + co] ^ 0x80008000u, s.u[1] = m[128 + co + 1] ^ 0x80008000u;
+        s.v[0] = m[160 + co] ^ 0x80008000u, s.v[1] = m[160 + co + 1] ^ 0x80008000u;
+      } else if (!kDecode) {
         const uint4* ry = (const uint4*)(a.in.y + (size_t)(py + gi) * a.wa + px);
         const uint4 r0 = ry[0], r1 = ry[1];
         s.y[0] = r0.x, s.y[1] = r0.y, s.y[2] = r0.z, s.y[3] = r0.w;
@@ -2481,7 +2540,13 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // searches: live across them, they pushed the engine into scratch
       // spills
       int svp[2] = {0, 0};
-      if (!kDecode) {
+      if (!kDecode && kSrcDma) {
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+          int pl, ex, ey;
+          elem_coords((wave + 4 * bi) * 64 + lane, 0, 0, pl, ex, ey);
+          svp[bi] = L.src[bx & 1][pl == 0 ? ey * 16 + ex : 256 + (pl - 1) * 64 + ey * 8 + ex];
+        }
+      } else if (!kDecode) {
         _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
           int pl, ex, ey;
           elem_coords((wave + 4 * bi) * 64 + lane, px, py, pl, ex, ey);
@@ -2603,6 +2668,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
       if (tid == 0 && !kDecode) a.table[mb] = d;
+      if (kSrcDma == 2 && !kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
       // every wave's coefficient stores drained, then the block info for the
       // deblock (its edge strengths); thread 0's drain covers only wave 0, so
       // the other waves drain before the barrier of the next macroblock --
