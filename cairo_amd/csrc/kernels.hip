@@ -456,8 +456,17 @@ __device__ __forceinline__ uint4 bias4(uint4 v) {
 #endif
 constexpr int kWinUnroll = CAIRO_WIN_UNROLL;
 
+// Traffic attribution builds (tools/attr_traffic.sh; never a product build):
+// bit 0 skips the search-window loads (the windows hold stale LDS), bit 2 the
+// row coder's inter-prediction loads (constant predictions).  The searches and
+// codes then run on wrong data -- same task shapes, wrong results -- so the
+// drop in fabric reads against the default build is what those loads cost.
+#ifndef CAIRO_ATTR_SKIP
+#define CAIRO_ATTR_SKIP 0
+#endif
 __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa, int ha, int ox,
                                             int oy, int r0, int r1, int c0, int c1) {
+  if (CAIRO_ATTR_SKIP & 1) return;
   // All of a thread's 16-byte loads are issued before the first LDS store
   // (kWinUnroll in flight): the staging costs one fabric round trip instead
   // of one per chunk.  Chunks are numbered over whole window rows (16 per
@@ -522,6 +531,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void dma_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
                                            int r1, int c0, int c1) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (CAIRO_ATTR_SKIP & 1) return;
   if (CAIRO_WIN_DMA == 2) {
     // 16-byte lanes: the window's rows are numbered as 16-byte chunks over the
     // PADDED pitch (17 per luma row, 9 per chroma row), so one wave
@@ -2153,6 +2163,7 @@ __device__ __forceinline__ const int16_t* plane_of(const PlaneSet& p, int pl) {
 // plane set p, lerped toward (mx+dx, my+dy) when sp (macroblock.h:203-259).
 __device__ __forceinline__ int pred_global(const PlaneSet& p, int wa, int e, int mx, int my, bool sp,
                                            int dx, int dy, int amount) {
+  if (CAIRO_ATTR_SKIP & 4) return 128;
   int pl, ex, ey;
   elem_coords(e, mx, my, pl, ex, ey);
   const int pitch = pl == 0 ? wa : (wa >> 1);
