@@ -1934,6 +1934,17 @@ struct alignas(16) RowWindow {
 #endif
 constexpr int kSrcDma = CAIRO_SRC_DMA;
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+// A macroblock's info granule (which tells the deblock that its coefficient
+// stores are visible) published by the NEXT macroblock, after the barrier in
+// front of its search: every wave has by then waited for all its stores at the
+// source-prefetch wait (kSrcDma == 1), so the macroblock's own end needs no
+// vmcnt(0) drain of them and the store round trip overlaps the next
+// macroblock's granule round trip instead of preceding it.  The row's last
+// macroblock drains and publishes at the row end.  Measured -0.7 % at 4K
+// (the later info delays the deblock, hence the next frame's helpers): off.
+#ifndef CAIRO_LATE_INFO
+#define CAIRO_LATE_INFO 0
+#endif
 
 struct alignas(16) RowLds {
   RowWindow win;
@@ -2244,6 +2255,8 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
   const int mbs = a.wmb * a.hmb;
+  constexpr bool late_info = CAIRO_LATE_INFO && kSrcDma == 1 && !kDecode && !kCoderDeblock;
+  uint64_t info = 0;  // late_info: the previous macroblock's info granule, published after the next barrier
 #if CAIRO_CODER_DEBLOCK
   DbState dst{0, 0, 0, 8};
 #endif
@@ -2428,6 +2441,8 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       if (!early) load_inter();
       stamp(a, mb, 1);
       __syncthreads();
+      // macroblock bx-1's info: all its stores waited for by every wave (above)
+      if (late_info && bx > 0 && tid == 0) gran_st(gran_at(a, bx - 1, by, kGranulesPerMB), info);
       stamp(a, mb, 2);
       tacc = acct_now();
 
@@ -2685,14 +2700,18 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // the other waves drain before the barrier of the next macroblock --
       // the deblock reads their coefficients only through this granule, hence
       // the barrier: info after all four waves drained
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0)
-        gran_st(gran_at(a, bx, by, kGranulesPerMB),
-                ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index);
+      info = ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index;
+      if (!late_info) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // (late_info: the LDS reuse of the next macroblock; no drain)
+      if (!late_info && tid == 0) gran_st(gran_at(a, bx, by, kGranulesPerMB), info);
       stamp(a, mb, 9);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
+  }
+  if (late_info) {  // the row's last macroblock
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) gran_st(gran_at(a, a.wmb - 1, by, kGranulesPerMB), info);
   }
 #if CAIRO_CODER_DEBLOCK
   // the rest of the row's deblock (each chunk waits for the row above)
