@@ -1933,6 +1933,14 @@ struct alignas(16) RowWindow {
 #define CAIRO_SRC_DMA 1
 #endif
 constexpr int kSrcDma = CAIRO_SRC_DMA;
+// The row coder's integer intra-search stages evaluated by every wave for
+// itself (1: each wave 9 candidates in 3 passes, gathered by ds_bpermute; no
+// barrier per stage) or spread over the workgroup's 16 lane groups with an
+// LDS exchange and a barrier per stage (0).
+#ifndef CAIRO_INTRA_WAVE
+#define CAIRO_INTRA_WAVE 1
+#endif
+constexpr bool kIntraWave = CAIRO_INTRA_WAVE;
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 // A macroblock's info granule (which tells the deblock that its coefficient
 // stores are visible) published by the NEXT macroblock, after the barrier in
@@ -2469,6 +2477,30 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           const int step = stage == 0 ? kRadius : (kRadius >> stage);
           const int jlo = stage == 0 ? -2 * kRadius : -step;
           const int bx0 = sel.bx, by0 = sel.by;
+          if (kIntraWave) {
+            // every wave evaluates the stage's 9 candidates itself, in 3 passes
+            // of its four 16-lane groups (pass p, group q -> candidate 4p + q),
+            // and lane c < 9 gathers candidate c (ds_bpermute from lane
+            // 16 (c & 3)): the waves replay the same selection, no LDS
+            // exchange and no workgroup barrier per stage
+            const int q = lane >> 4, c = lane & 15;
+            int vs = -1, vm = 0;
+#pragma unroll
+            for (int p = 0; p < 3; p++) {
+              const int k = min(4 * p + q, 8);
+              const int cx = bx0 - step + (k % 3) * step, cy = by0 + jlo + (k / 3) * step;
+              const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
+              int sad, mad;
+              cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
+              const int from = (16 * (c & 3)) << 2;
+              const int ps = __builtin_amdgcn_ds_bpermute(from, ok ? sad : -1);
+              const int pm = __builtin_amdgcn_ds_bpermute(from, mad);
+              if ((c >> 2) == p) vs = ps, vm = pm;
+            }
+            const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
+            select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
+            continue;
+          }
           {  // group g < 9 evaluates candidate g; groups 9..15 repeat candidate 8
             const int c = min(grp, 8);
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
