@@ -1936,11 +1936,20 @@ constexpr int kSrcDma = CAIRO_SRC_DMA;
 // The row coder's integer intra-search stages evaluated by every wave for
 // itself (1: each wave 9 candidates in 3 passes, gathered by ds_bpermute; no
 // barrier per stage) or spread over the workgroup's 16 lane groups with an
-// LDS exchange and a barrier per stage (0).
+// LDS exchange and a barrier per stage (0).  1 measured -21 % at 4K: three
+// times the LDS reads and VALU work of the search in every wave; the coders
+// are bound by the CU's LDS / VALU throughput there, not only by latency.
 #ifndef CAIRO_INTRA_WAVE
-#define CAIRO_INTRA_WAVE 1
+#define CAIRO_INTRA_WAVE 0
 #endif
 constexpr bool kIntraWave = CAIRO_INTRA_WAVE;
+// The 16 lane groups of the workgroup cover a stage's 9 candidates; groups
+// 9..15 (the top of wave 2 and all of wave 3) idle instead of repeating
+// candidate 8 (0): 7/16 of the stage's LDS reads and VALU work saved.
+#ifndef CAIRO_INTRA_IDLE
+#define CAIRO_INTRA_IDLE 1
+#endif
+constexpr bool kIntraIdle = CAIRO_INTRA_IDLE;
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 // A macroblock's info granule (which tells the deblock that its coefficient
 // stores are visible) published by the NEXT macroblock, after the barrier in
@@ -2501,7 +2510,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
             select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
             continue;
           }
-          {  // group g < 9 evaluates candidate g; groups 9..15 repeat candidate 8
+          if (!kIntraIdle || grp < 9) {  // group g < 9 evaluates candidate g (kIntraIdle: groups 9..15 idle)
             const int c = min(grp, 8);
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
