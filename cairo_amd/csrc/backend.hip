@@ -457,8 +457,7 @@ int zero_state(cairo_ctx* c) {
   for (int k = 0; k < c->coef_chunks; k++)
     CK(hipMemsetAsync(c->coef[k], 0, c->plane_elems * 2 * (size_t)std::min(c->coef_per, c->stages - k * c->coef_per),
                       c->ks));
-  // the zero image in the planes' storage domain (kBiasedRecon: 0x8000)
-  CK(hipMemsetD16Async((hipDeviceptr_t)c->ring_buf, kBiasedRecon ? 0x8000 : 0, c->plane_elems * c->ring_slots, c->ks));
+  CK(hipMemsetAsync(c->ring_buf, 0, c->plane_elems * 2 * c->ring_slots, c->ks));
   CK(hipMemsetAsync(c->table, 0, c->mbs * sizeof(BlockDesc) * S, c->ks));
   // inter records: a frame whose search was cut short by a timed-out wait
   // still reads in-frame motion vectors
@@ -1506,7 +1505,7 @@ int cairo_ctx_join_group(cairo_ctx* c, int size, int rank, const cairo_peer* pee
   // time their cost on one device)
   c->sys = sys || getenv("CAIRO_GROUP_FORCE_SYS") != nullptr;
   CK(hipMalloc(&c->zero, c->plane_elems * 2));
-  CK(hipMemsetD16((hipDeviceptr_t)c->zero, kBiasedRecon ? 0x8000 : 0, c->plane_elems));
+  CK(hipMemset(c->zero, 0, c->plane_elems * 2));
   // a member's consecutive frames are N stream frames apart
   return upload_orders(c, 3 * size + 2);
 }
@@ -1541,11 +1540,6 @@ int cairo_ctx_read_planes(cairo_ctx* c, int which, int16_t* y, int16_t* u, int16
   if (y) CK(hipMemcpy(y, p.y, ly * 2, hipMemcpyDeviceToHost));
   if (u) CK(hipMemcpy(u, p.u, lc * 2, hipMemcpyDeviceToHost));
   if (v) CK(hipMemcpy(v, p.v, lc * 2, hipMemcpyDeviceToHost));
-  if (which >= 2 && kBiasedRecon) {  // reconstruction slots are stored biased (kernels.h)
-    for (size_t i = 0; y && i < ly; i++) y[i] = recon_unbias(y[i]);
-    for (size_t i = 0; u && i < lc; i++) u[i] = recon_unbias(u[i]);
-    for (size_t i = 0; v && i < lc; i++) v[i] = recon_unbias(v[i]);
-  }
   return kSuccess;
 }
 

@@ -44,18 +44,6 @@ constexpr int kGranuleStride = 193;   // + info granule
 #ifndef CAIRO_TAGGED_RECORDS
 #define CAIRO_TAGGED_RECORDS 1
 #endif
-// Reconstructed reference planes (the ring slots, the readers' mirrors and
-// the zero image) stored biased in HBM, v ^ 0x8000 (unsigned order = signed
-// order), the domain the searches compare in: the search windows are staged
-// as they are (no biasing pass over LDS after an LDS-DMA), and the few
-// element-wise readers (deblock rows above, zero-MV, predictions, YUV->RGB,
-// cairo_ctx_read_planes) unbias.  0: plain int16 planes.
-#ifndef CAIRO_BIASED_RECON
-#define CAIRO_BIASED_RECON 1
-#endif
-constexpr bool kBiasedRecon = CAIRO_BIASED_RECON;
-constexpr uint32_t kReconBias2 = kBiasedRecon ? 0x80008000u : 0u;  // xor of a stored pixel pair
-__host__ __device__ inline int16_t recon_unbias(int16_t v) { return kBiasedRecon ? (int16_t)(v ^ (int16_t)0x8000) : v; }
 __host__ __device__ inline uint32_t pack_inter_desc(const BlockDesc& d) {
   return (d.block_type & 7u) | ((uint32_t)(d.prediction_target & 3) << 3) | ((uint32_t)(d.sp_pred & 1) << 5) |
          ((uint32_t)(d.sp_amount & 1) << 6) | ((uint32_t)(d.sp_index & 15) << 7) |

@@ -503,7 +503,7 @@ __device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa
 #pragma unroll
     for (int u = 0; u < kWinUnroll; u++)
       if (dst[u]) {
-        const uint4 b = kBiasedRecon ? v[u] : bias4(v[u]);  // (biased planes: as stored)
+        const uint4 b = bias4(v[u]);
         if (kWinLP % 8 == 0) {
           *(uint4*)dst[u] = b;
         } else {  // 8-byte aligned rows (chroma rows stay 16-byte aligned; the same stores serve both)
@@ -614,7 +614,7 @@ __device__ __forceinline__ void load_window_dma(Window& w, const PlaneSet& p, in
   dma_window(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
   __syncthreads();                                    // ... every wave's
-  if (!kBiasedRecon) bias_window(w, r0, r1, c0, c1);
+  bias_window(w, r0, r1, c0, c1);
 }
 
 __device__ __forceinline__ void acct_window(uint64_t* acct, int r0, int r1, int c0, int c1) {
@@ -650,16 +650,6 @@ __device__ __forceinline__ Px6 px_from_window_b(const Window& w, int wx, int wy)
   return r;
 }
 
-__device__ __forceinline__ Px6 px_from_planes(const PlaneSet& p, int wa, int x, int y);
-// This lane's Px6 slice of a reconstructed reference (kBiasedRecon: unbiased).
-__device__ __forceinline__ Px6 px_from_ref(const PlaneSet& p, int wa, int x, int y) {
-  Px6 r = px_from_planes(p, wa, x, y);
-  if (kBiasedRecon) {
-    r.y0 = recon_unbias((int16_t)r.y0), r.y1 = recon_unbias((int16_t)r.y1), r.y2 = recon_unbias((int16_t)r.y2);
-    r.y3 = recon_unbias((int16_t)r.y3), r.u = recon_unbias((int16_t)r.u), r.v = recon_unbias((int16_t)r.v);
-  }
-  return r;
-}
 __device__ __forceinline__ Px6 px_from_planes(const PlaneSet& p, int wa, int x, int y) {
   int l = lane_id();
   const int16_t* py = &p.y[(size_t)(y + (l >> 2)) * wa + x + (l & 3) * 4];
@@ -1125,7 +1115,7 @@ __device__ __forceinline__ void zero_mv_older(FA& a, int r, int g, InterLds& L) 
   Px6 ref[kMaxRing - 1];
 #pragma unroll
   for (int off = 2; off < kMaxRing; off++)
-    if (off <= a.nref) ref[off - 1] = px_from_ref(RECON_AT(a, off), a.wa, px, py);
+    if (off <= a.nref) ref[off - 1] = px_from_planes(RECON_AT(a, off), a.wa, px, py);
 #pragma unroll
   for (int off = 2; off < kMaxRing; off++) {
     if (off > a.nref) break;
@@ -1180,11 +1170,11 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     if (off >= 2) {  // zero-MV computed at the group start
       s.sad = L.zsad[off][wave], s.mad = L.zmad[off][wave];
     } else {  // zero-MV candidate straight from the planes
-      sad_mad(src, px_from_ref(ref, a.wa, px, py), s.sad, s.mad);
+      sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
     }
   } else if (valid) {  // zero-MV candidate straight from the planes
     src = px_from_planes(planes(a.in), a.wa, px, py);
-    sad_mad(src, px_from_ref(ref, a.wa, px, py), s.sad, s.mad);
+    sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
     srow = load_src_rows(planes(a.in), a.wa, px, py, threadIdx.x & 15);
   }
   const bool need = valid && s.mad >= thr;
@@ -1223,7 +1213,7 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     const bool full = L.full != 0;  // workgroup-uniform
     acct_add(a.acct, Acct::kSearchedTasks, 1);
     acct_window(a.acct, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
-    if (staged && !kBiasedRecon)
+    if (staged)
       bias_window(L.win, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     else
       stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
@@ -1781,9 +1771,8 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
 #pragma unroll
           for (int u = 0; u < kAbove; u++)
             if (dst[u]) {
-              const uint32_t x = v[u] ^ kReconBias2;
-              dst[u][0] = (int16_t)(x & 0xFFFF);
-              dst[u][1] = (int16_t)(x >> 16);
+              dst[u][0] = (int16_t)(v[u] & 0xFFFF);
+              dst[u][1] = (int16_t)(v[u] >> 16);
             }
           }
         }
@@ -1865,7 +1854,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           g = pick(cs, 1 + pj) + (size_t)(c0y + row) * cw + col;
         }
         const int16_t* p = db_px(D, pl, row, col);
-        const uint32_t d = ((uint32_t)(uint16_t)p[0] | ((uint32_t)(uint16_t)p[1] << 16)) ^ kReconBias2;
+        const uint32_t d = (uint32_t)(uint16_t)p[0] | ((uint32_t)(uint16_t)p[1] << 16);
         __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)g, d, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         const size_t off = (size_t)(g - pick(cs, pl));
@@ -2207,11 +2196,11 @@ __device__ __forceinline__ int pred_global(const PlaneSet& p, int wa, int e, int
   elem_coords(e, mx, my, pl, ex, ey);
   const int pitch = pl == 0 ? wa : (wa >> 1);
   const int16_t* t = plane_of(p, pl);
-  int v = recon_unbias(t[(size_t)ey * pitch + ex]);
+  int v = t[(size_t)ey * pitch + ex];
   if (sp) {
     int nx, ny;
     elem_coords(e, mx + dx, my + dy, pl, nx, ny);
-    v = lerp_px(v, recon_unbias(t[(size_t)ny * pitch + nx]), amount);
+    v = lerp_px(v, t[(size_t)ny * pitch + nx], amount);
   }
   return v;
 }
@@ -2410,7 +2399,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       if (tid < kGranulesPerMB) {
         if (pf3) pg3 = gran_ld(gran_at(a, bx + 3, by - 3, tid));
         if (pf2) pg2 = gran_ld(gran_at(a, bx + 3, by - 2, tid));
-        if (pfs && !early) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid) ^ kReconBias2;  // (early: after the wait)
+        if (pfs && !early) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);  // (early: after the wait)
       }
 
       // ---- inter predictions, prefetched (the K1 records are final) ----
@@ -2576,7 +2565,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           __syncthreads();
           acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
           tacc = acct_now();
-          if (tid < kGranulesPerMB && pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid) ^ kReconBias2;
+          if (tid < kGranulesPerMB && pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);
           load_inter();
           acct_add(a.acct, Acct::kCoderInter, acct_now() - tacc);
         }
@@ -3203,12 +3192,12 @@ __device__ __forceinline__ uint8_t sat8(int32_t v) {
 __global__ __launch_bounds__(256) void k_yuv_to_rgb(PlaneSet src, int wa, int w, int h, uint8_t* rgb) {
   const int x2 = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
   if (2 * x2 >= w) return;
-  const int u = recon_unbias(src.u[(size_t)(y >> 1) * (wa >> 1) + x2]) - 128;
-  const int v = recon_unbias(src.v[(size_t)(y >> 1) * (wa >> 1) + x2]) - 128;
+  const int u = src.u[(size_t)(y >> 1) * (wa >> 1) + x2] - 128;
+  const int v = src.v[(size_t)(y >> 1) * (wa >> 1) + x2] - 128;
   uint8_t* o = rgb + ((size_t)y * w + 2 * x2) * 3;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
-    const int yy = recon_unbias(src.y[(size_t)y * wa + 2 * x2 + k]) - 16;
+    const int yy = src.y[(size_t)y * wa + 2 * x2 + k] - 16;
     o[3 * k] = sat8((256 * yy + 358 * v + 128) >> 8);
     o[3 * k + 1] = sat8((256 * yy - 88 * u - 182 * v + 128) >> 8);
     o[3 * k + 2] = sat8((256 * yy + 452 * u + 128) >> 8);
