@@ -1950,6 +1950,15 @@ constexpr bool kIntraWave = CAIRO_INTRA_WAVE;
 #define CAIRO_INTRA_IDLE 1
 #endif
 constexpr bool kIntraIdle = CAIRO_INTRA_IDLE;
+// Stages 1-4 of the intra search: the 3x3's centre (candidate 4) is the
+// current best, whose SAD and MAD the state holds (same position, same source,
+// same window), or the macroblock's own position while nothing was accepted
+// (not yet coded: not offered).  So only 8 candidates are evaluated, by waves
+// 0 and 1, and waves 2 and 3 idle (stage 0's grid is offset: 9 candidates).
+#ifndef CAIRO_INTRA_CENTRE
+#define CAIRO_INTRA_CENTRE 1
+#endif
+constexpr bool kIntraCentre = CAIRO_INTRA_CENTRE;
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 // A macroblock's info granule (which tells the deblock that its coefficient
 // stores are visible) published by the NEXT macroblock, after the barrier in
@@ -2510,21 +2519,25 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
             select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
             continue;
           }
-          if (!kIntraIdle || grp < 9) {  // group g < 9 evaluates candidate g (kIntraIdle: groups 9..15 idle)
-            const int c = min(grp, 8);
+          const bool centre = kIntraCentre && stage > 0;  // workgroup-uniform
+          if (centre ? grp < 8 : (!kIntraIdle || grp < 9)) {
+            // group g < 9 evaluates candidate g (kIntraIdle: groups 9..15 idle);
+            // with the centre known, groups 0..7 candidates 0..3, 5..8
+            const int c = centre ? grp + (grp >= 4) : min(grp, 8);
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
             int sad, mad;
             cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
-            if (gi == 0 && grp < 9) {
-              L.cand[buf][grp][0] = ok ? sad : -1;
-              L.cand[buf][grp][1] = mad;
+            if (gi == 0 && (centre || grp < 9)) {
+              L.cand[buf][c][0] = ok ? sad : -1;
+              L.cand[buf][c][1] = mad;
             }
           }
           __syncthreads();
           {
             const int c = lane & 15;
-            const int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
+            int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
+            if (centre && c == 4) vs = sel.mad != INT32_MAX ? sel.sad : -1, vm = sel.mad;
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
           }
