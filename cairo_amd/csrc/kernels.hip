@@ -1955,8 +1955,9 @@ constexpr bool kIntraIdle = CAIRO_INTRA_IDLE;
 // same window), or the macroblock's own position while nothing was accepted
 // (not yet coded: not offered).  So only 8 candidates are evaluated, by waves
 // 0 and 1, and waves 2 and 3 idle (stage 0's grid is offset: 9 candidates).
+// Bit-exact (GPU suite green) but measured -1.1 % at 4K (one round): off.
 #ifndef CAIRO_INTRA_CENTRE
-#define CAIRO_INTRA_CENTRE 1
+#define CAIRO_INTRA_CENTRE 0
 #endif
 constexpr bool kIntraCentre = CAIRO_INTRA_CENTRE;
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
