@@ -1933,16 +1933,7 @@ struct alignas(16) RowWindow {
 #define CAIRO_SRC_DMA 1
 #endif
 constexpr int kSrcDma = CAIRO_SRC_DMA;
-// The row coder's integer intra-search stages evaluated by every wave for
-// itself (1: each wave 9 candidates in 3 passes, gathered by ds_bpermute; no
-// barrier per stage) or spread over the workgroup's 16 lane groups with an
-// LDS exchange and a barrier per stage (0).  1 measured -21 % at 4K: three
-// times the LDS reads and VALU work of the search in every wave; the coders
-// are bound by the CU's LDS / VALU throughput there, not only by latency.
-#ifndef CAIRO_INTRA_WAVE
-#define CAIRO_INTRA_WAVE 0
-#endif
-constexpr bool kIntraWave = CAIRO_INTRA_WAVE;
+
 // The 16 lane groups of the workgroup cover a stage's 9 candidates; groups
 // 9..15 (the top of wave 2 and all of wave 3) idle instead of repeating
 // candidate 8 (0): 7/16 of the stage's LDS reads and VALU work saved.
@@ -1950,28 +1941,9 @@ constexpr bool kIntraWave = CAIRO_INTRA_WAVE;
 #define CAIRO_INTRA_IDLE 1
 #endif
 constexpr bool kIntraIdle = CAIRO_INTRA_IDLE;
-// Stages 1-4 of the intra search: the 3x3's centre (candidate 4) is the
-// current best, whose SAD and MAD the state holds (same position, same source,
-// same window), or the macroblock's own position while nothing was accepted
-// (not yet coded: not offered).  So only 8 candidates are evaluated, by waves
-// 0 and 1, and waves 2 and 3 idle (stage 0's grid is offset: 9 candidates).
-// Bit-exact (GPU suite green) but measured -1.1 % at 4K (one round): off.
-#ifndef CAIRO_INTRA_CENTRE
-#define CAIRO_INTRA_CENTRE 0
-#endif
-constexpr bool kIntraCentre = CAIRO_INTRA_CENTRE;
+
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
-// A macroblock's info granule (which tells the deblock that its coefficient
-// stores are visible) published by the NEXT macroblock, after the barrier in
-// front of its search: every wave has by then waited for all its stores at the
-// source-prefetch wait (kSrcDma == 1), so the macroblock's own end needs no
-// vmcnt(0) drain of them and the store round trip overlaps the next
-// macroblock's granule round trip instead of preceding it.  The row's last
-// macroblock drains and publishes at the row end.  Measured -0.7 % at 4K
-// (the later info delays the deblock, hence the next frame's helpers): off.
-#ifndef CAIRO_LATE_INFO
-#define CAIRO_LATE_INFO 0
-#endif
+
 
 struct alignas(16) RowLds {
   RowWindow win;
@@ -2282,8 +2254,6 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
   const int mbs = a.wmb * a.hmb;
-  constexpr bool late_info = CAIRO_LATE_INFO && kSrcDma == 1 && !kDecode && !kCoderDeblock;
-  uint64_t info = 0;  // late_info: the previous macroblock's info granule, published after the next barrier
 #if CAIRO_CODER_DEBLOCK
   DbState dst{0, 0, 0, 8};
 #endif
@@ -2468,8 +2438,6 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       if (!early) load_inter();
       stamp(a, mb, 1);
       __syncthreads();
-      // macroblock bx-1's info: all its stores waited for by every wave (above)
-      if (late_info && bx > 0 && tid == 0) gran_st(gran_at(a, bx - 1, by, kGranulesPerMB), info);
       stamp(a, mb, 2);
       tacc = acct_now();
 
@@ -2496,49 +2464,21 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           const int step = stage == 0 ? kRadius : (kRadius >> stage);
           const int jlo = stage == 0 ? -2 * kRadius : -step;
           const int bx0 = sel.bx, by0 = sel.by;
-          if (kIntraWave) {
-            // every wave evaluates the stage's 9 candidates itself, in 3 passes
-            // of its four 16-lane groups (pass p, group q -> candidate 4p + q),
-            // and lane c < 9 gathers candidate c (ds_bpermute from lane
-            // 16 (c & 3)): the waves replay the same selection, no LDS
-            // exchange and no workgroup barrier per stage
-            const int q = lane >> 4, c = lane & 15;
-            int vs = -1, vm = 0;
-#pragma unroll
-            for (int p = 0; p < 3; p++) {
-              const int k = min(4 * p + q, 8);
-              const int cx = bx0 - step + (k % 3) * step, cy = by0 + jlo + (k / 3) * step;
-              const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
-              int sad, mad;
-              cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
-              const int from = (16 * (c & 3)) << 2;
-              const int ps = __builtin_amdgcn_ds_bpermute(from, ok ? sad : -1);
-              const int pm = __builtin_amdgcn_ds_bpermute(from, mad);
-              if ((c >> 2) == p) vs = ps, vm = pm;
-            }
-            const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
-            select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
-            continue;
-          }
-          const bool centre = kIntraCentre && stage > 0;  // workgroup-uniform
-          if (centre ? grp < 8 : (!kIntraIdle || grp < 9)) {
-            // group g < 9 evaluates candidate g (kIntraIdle: groups 9..15 idle);
-            // with the centre known, groups 0..7 candidates 0..3, 5..8
-            const int c = centre ? grp + (grp >= 4) : min(grp, 8);
+          if (!kIntraIdle || grp < 9) {  // group g < 9 evaluates candidate g (kIntraIdle: groups 9..15 idle)
+            const int c = min(grp, 8);
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
             int sad, mad;
             cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
-            if (gi == 0 && (centre || grp < 9)) {
-              L.cand[buf][c][0] = ok ? sad : -1;
-              L.cand[buf][c][1] = mad;
+            if (gi == 0 && grp < 9) {
+              L.cand[buf][grp][0] = ok ? sad : -1;
+              L.cand[buf][grp][1] = mad;
             }
           }
           __syncthreads();
           {
             const int c = lane & 15;
-            int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
-            if (centre && c == 4) vs = sel.mad != INT32_MAX ? sel.sad : -1, vm = sel.mad;
+            const int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
           }
@@ -2755,18 +2695,14 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // the other waves drain before the barrier of the next macroblock --
       // the deblock reads their coefficients only through this granule, hence
       // the barrier: info after all four waves drained
-      info = ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index;
-      if (!late_info) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // (late_info: the LDS reuse of the next macroblock; no drain)
-      if (!late_info && tid == 0) gran_st(gran_at(a, bx, by, kGranulesPerMB), info);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        gran_st(gran_at(a, bx, by, kGranulesPerMB),
+                ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index);
       stamp(a, mb, 9);
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
-  }
-  if (late_info) {  // the row's last macroblock
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) gran_st(gran_at(a, a.wmb - 1, by, kGranulesPerMB), info);
   }
 #if CAIRO_CODER_DEBLOCK
   // the rest of the row's deblock (each chunk waits for the row above)
