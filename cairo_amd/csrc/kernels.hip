@@ -1025,6 +1025,14 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
 #define CAIRO_GROUP_SOURCE 1
 #endif
 constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
+// The row helper's group source double-buffered in LDS: group g+1's four
+// macroblocks staged by LDS-DMA (one instruction per wave) at group g's start,
+// in flight with g's progress poll whose wait covers them, instead of a
+// register load round trip at each group's start.
+#ifndef CAIRO_HSRC_DMA
+#define CAIRO_HSRC_DMA 1
+#endif
+constexpr bool kHelperSrcDma = CAIRO_HSRC_DMA && CAIRO_GROUP_SOURCE;
 // Window DMA issued before the zero-MV loads (one round trip for both), with
 // the whole-window finality taken from the preceding helper_wait (1), or
 // staged after the zero-MV check (0).
@@ -1041,7 +1049,7 @@ struct InterLds {
   // the group's source macroblocks (raw int16: 16x16 luma, 8x8 U, 8x8 V per
   // wave), loaded once per group; the zero-MV SAD / MAD of the older
   // references, computed together at the group start
-  alignas(16) int16_t src[4][384];
+  alignas(16) int16_t src[2][4][384];  // by group g & 1 (kHelperSrcDma: group g+1 staged during g)
   int zsad[kMaxRing][4], zmad[kMaxRing][4];
 };
 
@@ -1049,7 +1057,7 @@ struct InterLds {
 // 16 x 16, then U 8 x 8, then V 8 x 8; lanes 0..47 one 16-byte chunk each (a
 // luma half row, a chroma row).  Only this wave reads it back (its LDS
 // operations execute in order: no barrier).
-__device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L) {
+__device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L, bool dma = false) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, x = 4 * g + wave;
   if (x >= a.wmb || lane >= 48) return;
   const PlaneSet in = planes(a.in);
@@ -1061,7 +1069,10 @@ __device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L) {
     const int k = lane - 32;
     gsrc = pick(in, 1 + (k >> 3)) + (size_t)((py >> 1) + (k & 7)) * (a.wa >> 1) + (px >> 1);
   }
-  *(uint4*)&L.src[wave][8 * lane] = *(const uint4*)gsrc;
+  if (dma)  // one LDS-DMA instruction per wave: lane l lands at + 16 l, the layout above
+    __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)&L.src[g & 1][wave][0], 16, 0, 0);
+  else
+    *(uint4*)&L.src[g & 1][wave][8 * lane] = *(const uint4*)gsrc;
 }
 
 // Macroblock (x, r)'s source into dst (group_source's layout) by ONE LDS-DMA
@@ -1082,9 +1093,9 @@ __device__ __forceinline__ void src_dma(FA& a, int x, int r, int16_t* dst) {
 
 // This lane's Px6 slice (px_from_planes layout) and its SrcRow (load_src_rows
 // layout, biased) of wave w's source macroblock, from L.src.
-__device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int wave) {
+__device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
   const int l = threadIdx.x & 63;
-  const int16_t* m = L.src[wave];
+  const int16_t* m = L.src[g & 1][wave];
   Px6 p;
   const int16_t* y = &m[(l >> 2) * 16 + (l & 3) * 4];
   p.y0 = y[0], p.y1 = y[1], p.y2 = y[2], p.y3 = y[3];
@@ -1092,8 +1103,8 @@ __device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int wave) {
   p.v = m[320 + (l >> 3) * 8 + (l & 7)];
   return p;
 }
-__device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int wave, int i) {
-  const uint32_t* m = (const uint32_t*)L.src[wave];
+__device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int g, int wave, int i) {
+  const uint32_t* m = (const uint32_t*)L.src[g & 1][wave];
   SrcRow s;
 #pragma unroll
   for (int k = 0; k < 8; k++) s.y[k] = m[i * 8 + k] ^ 0x80008000u;
@@ -1111,7 +1122,7 @@ __device__ __forceinline__ void zero_mv_older(FA& a, int r, int g, InterLds& L) 
   acct_add(a.acct, Acct::kZeroMvBytes, 768ull * (a.nref - 1) * (uint64_t)min(4, a.wmb - 4 * g));
   if (x >= a.wmb) return;
   const int px = x * kMB, py = r * kMB;
-  const Px6 src = src_px_lds(L, wave);
+  const Px6 src = src_px_lds(L, g, wave);
   Px6 ref[kMaxRing - 1];
 #pragma unroll
   for (int off = 2; off < kMaxRing; off++)
@@ -1165,8 +1176,8 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     staged = true;
   }
   if (valid && kGroupSource) {  // the source from the group's LDS copy
-    src = src_px_lds(L, wave);
-    srow = src_rows_lds(L, wave, threadIdx.x & 15);
+    src = src_px_lds(L, g, wave);
+    srow = src_rows_lds(L, g, wave, threadIdx.x & 15);
     if (off >= 2) {  // zero-MV computed at the group start
       s.sad = L.zsad[off][wave], s.mad = L.zmad[off][wave];
     } else {  // zero-MV candidate straight from the planes
@@ -2747,7 +2758,19 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     // progress word, tagged epoch-2, also covers frame index-3: that frame's
     // row r+2 waited for index-3's row r+4 over a wider window), so these
     // searches fill what used to be the wait for the previous frame.
-    if (kGroupSource && a.inter) group_source(a, r, g, L.inter);
+    if (kGroupSource && a.inter) {
+      if (!kHelperSrcDma) {
+        group_source(a, r, g, L.inter);
+      } else {
+        if (g == 0) {  // the row's first group: staged here and waited for
+          group_source(a, r, 0, L.inter, true);
+          __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        }
+        // group g+1 (into the buffer group g-1 used; each wave reads only its
+        // own macroblock's source, so its own vmcnt waits cover its DMA)
+        if (g + 1 < a.ng) group_source(a, r, g + 1, L.inter, true);
+      }
+    }
     if (a.inter && a.nref >= 2) {
       helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag,
                   kSpecStage ? &L.inter.full : nullptr, inter_need_cols(a, g, 2));
