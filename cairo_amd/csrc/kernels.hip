@@ -1954,6 +1954,14 @@ constexpr int kSrcDma = CAIRO_SRC_DMA;
 constexpr bool kIntraIdle = CAIRO_INTRA_IDLE;
 
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+// A macroblock's end waits only for its coefficient stores (which its info
+// granule releases to the deblock and, through its progress, to the next
+// frame's copy macroblocks), not for the pixel-granule and table stores
+// issued after them (1), or for everything (0).
+#ifndef CAIRO_COEF_DRAIN
+#define CAIRO_COEF_DRAIN 1
+#endif
+constexpr bool kCoefDrain = CAIRO_COEF_DRAIN;
 
 
 struct alignas(16) RowLds {
@@ -2699,14 +2707,25 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
                     gran_settle(a, gran_at(a, bx + 3, by - 2, tid), pg2, by));
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
-      if (tid == 0 && !kDecode) a.table[mb] = d;
+      if (tid == 0 && !kDecode) *(uint4*)&a.table[mb] = __builtin_bit_cast(uint4, d);  // one 16-byte store
       if (kSrcDma == 2 && !kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
       // every wave's coefficient stores drained, then the block info for the
       // deblock (its edge strengths); thread 0's drain covers only wave 0, so
       // the other waves drain before the barrier of the next macroblock --
       // the deblock reads their coefficients only through this granule, hence
       // the barrier: info after all four waves drained
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (kCoefDrain && !kDecode) {
+        // only the coefficient stores: after them each wave issued its pixel
+        // granule stores (one per block: wave 0 and 1 two, waves 2 and 3
+        // one) and wave 0 the table store, which need no drain (tag-polled;
+        // read after the launch), and vmcnt retires in order.  More
+        // operations after them (stamps, accounting) only wait longer.
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else if (wave == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __syncthreads();
       if (tid == 0)
         gran_st(gran_at(a, bx, by, kGranulesPerMB),
