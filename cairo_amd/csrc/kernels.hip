@@ -1028,9 +1028,11 @@ constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
 // The row helper's group source double-buffered in LDS: group g+1's four
 // macroblocks staged by LDS-DMA (one instruction per wave) at group g's start,
 // in flight with g's progress poll whose wait covers them, instead of a
-// register load round trip at each group's start.
+// register load round trip at each group's start.  Bit-exact, measured
+// neutral at 4K (5784 vs 5782, profiles/r04/ab_4k_n.txt): off, and then the
+// second buffer is not allocated.
 #ifndef CAIRO_HSRC_DMA
-#define CAIRO_HSRC_DMA 1
+#define CAIRO_HSRC_DMA 0
 #endif
 constexpr bool kHelperSrcDma = CAIRO_HSRC_DMA && CAIRO_GROUP_SOURCE;
 // Window DMA issued before the zero-MV loads (one round trip for both), with
@@ -1049,7 +1051,7 @@ struct InterLds {
   // the group's source macroblocks (raw int16: 16x16 luma, 8x8 U, 8x8 V per
   // wave), loaded once per group; the zero-MV SAD / MAD of the older
   // references, computed together at the group start
-  alignas(16) int16_t src[2][4][384];  // by group g & 1 (kHelperSrcDma: group g+1 staged during g)
+  alignas(16) int16_t src[kHelperSrcDma ? 2 : 1][4][384];  // kHelperSrcDma: by group g & 1 (g+1 staged during g)
   int zsad[kMaxRing][4], zmad[kMaxRing][4];
 };
 
@@ -1070,9 +1072,9 @@ __device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L, b
     gsrc = pick(in, 1 + (k >> 3)) + (size_t)((py >> 1) + (k & 7)) * (a.wa >> 1) + (px >> 1);
   }
   if (dma)  // one LDS-DMA instruction per wave: lane l lands at + 16 l, the layout above
-    __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)&L.src[g & 1][wave][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)&L.src[g & kHelperSrcDma][wave][0], 16, 0, 0);
   else
-    *(uint4*)&L.src[g & 1][wave][8 * lane] = *(const uint4*)gsrc;
+    *(uint4*)&L.src[g & kHelperSrcDma][wave][8 * lane] = *(const uint4*)gsrc;
 }
 
 // Macroblock (x, r)'s source into dst (group_source's layout) by ONE LDS-DMA
@@ -1095,7 +1097,7 @@ __device__ __forceinline__ void src_dma(FA& a, int x, int r, int16_t* dst) {
 // layout, biased) of wave w's source macroblock, from L.src.
 __device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
   const int l = threadIdx.x & 63;
-  const int16_t* m = L.src[g & 1][wave];
+  const int16_t* m = L.src[g & kHelperSrcDma][wave];
   Px6 p;
   const int16_t* y = &m[(l >> 2) * 16 + (l & 3) * 4];
   p.y0 = y[0], p.y1 = y[1], p.y2 = y[2], p.y3 = y[3];
@@ -1104,7 +1106,7 @@ __device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
   return p;
 }
 __device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int g, int wave, int i) {
-  const uint32_t* m = (const uint32_t*)L.src[g & 1][wave];
+  const uint32_t* m = (const uint32_t*)L.src[g & kHelperSrcDma][wave];
   SrcRow s;
 #pragma unroll
   for (int k = 0; k < 8; k++) s.y[k] = m[i * 8 + k] ^ 0x80008000u;
