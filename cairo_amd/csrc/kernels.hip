@@ -1042,16 +1042,6 @@ constexpr bool kHelperSrcDma = CAIRO_HSRC_DMA && CAIRO_GROUP_SOURCE;
 #define CAIRO_SPEC_STAGE 0
 #endif
 constexpr bool kSpecStage = CAIRO_SPEC_STAGE && CAIRO_WIN_DMA != 0 && CAIRO_GROUP_SOURCE;
-// The row helper fills its wait for the previous frame at group g with group
-// g+1's older-reference searches (they read only frames index-2 and older),
-// one reference at a time, polling between them whether the previous frame
-// has arrived (then group g's reference-1 search, which the row coder waits
-// for, goes first).  Needs the group source double-buffered (g & 1).
-#ifndef CAIRO_HELPER_FILL
-#define CAIRO_HELPER_FILL 1
-#endif
-constexpr bool kHelperFill = CAIRO_HELPER_FILL && CAIRO_GROUP_SOURCE && !kSpecStage && !kHelperSrcDma;
-constexpr int kSrcBufMask = (kHelperSrcDma || kHelperFill) ? 1 : 0;  // group source buffer of group g: g & mask
 
 struct InterLds {
   Window win;
@@ -1061,7 +1051,7 @@ struct InterLds {
   // the group's source macroblocks (raw int16: 16x16 luma, 8x8 U, 8x8 V per
   // wave), loaded once per group; the zero-MV SAD / MAD of the older
   // references, computed together at the group start
-  alignas(16) int16_t src[kSrcBufMask + 1][4][384];  // by group g & kSrcBufMask (two groups live: kHelperSrcDma, kHelperFill)
+  alignas(16) int16_t src[kHelperSrcDma ? 2 : 1][4][384];  // kHelperSrcDma: by group g & 1 (g+1 staged during g)
   int zsad[kMaxRing][4], zmad[kMaxRing][4];
 };
 
@@ -1082,9 +1072,9 @@ __device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L, b
     gsrc = pick(in, 1 + (k >> 3)) + (size_t)((py >> 1) + (k & 7)) * (a.wa >> 1) + (px >> 1);
   }
   if (dma)  // one LDS-DMA instruction per wave: lane l lands at + 16 l, the layout above
-    __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)&L.src[g & kSrcBufMask][wave][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)&L.src[g & kHelperSrcDma][wave][0], 16, 0, 0);
   else
-    *(uint4*)&L.src[g & kSrcBufMask][wave][8 * lane] = *(const uint4*)gsrc;
+    *(uint4*)&L.src[g & kHelperSrcDma][wave][8 * lane] = *(const uint4*)gsrc;
 }
 
 // Macroblock (x, r)'s source into dst (group_source's layout) by ONE LDS-DMA
@@ -1107,7 +1097,7 @@ __device__ __forceinline__ void src_dma(FA& a, int x, int r, int16_t* dst) {
 // layout, biased) of wave w's source macroblock, from L.src.
 __device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
   const int l = threadIdx.x & 63;
-  const int16_t* m = L.src[g & kSrcBufMask][wave];
+  const int16_t* m = L.src[g & kHelperSrcDma][wave];
   Px6 p;
   const int16_t* y = &m[(l >> 2) * 16 + (l & 3) * 4];
   p.y0 = y[0], p.y1 = y[1], p.y2 = y[2], p.y3 = y[3];
@@ -1116,7 +1106,7 @@ __device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
   return p;
 }
 __device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int g, int wave, int i) {
-  const uint32_t* m = (const uint32_t*)L.src[g & kSrcBufMask][wave];
+  const uint32_t* m = (const uint32_t*)L.src[g & kHelperSrcDma][wave];
   SrcRow s;
 #pragma unroll
   for (int k = 0; k < 8; k++) s.y[k] = m[i * 8 + k] ^ 0x80008000u;
@@ -2769,18 +2759,6 @@ struct EngineLds {
   int flag;  // helper decisions broadcast from thread 0 (kept out of the union)
 };
 
-// Whether the previous frame is final over group g's level-1 window (the
-// condition of helper_wait back 1), without waiting: one poll by thread 0,
-// broadcast.  No acquire: the caller waits (and acquires) before reading.
-__device__ __forceinline__ bool prev_ready(FA& a, int r, int g, int* flag) {
-  int d = 0;
-  if (threadIdx.x == 0) {
-    const uint64_t* pp = a.prev_progress;
-    d = !pp || progress_peer(a.sys, pp + min(r + 2, a.hmb - 1)) >= tagged(a.epoch - 1, inter_need_cols(a, g, 1));
-  }
-  return wg_broadcast((volatile int*)flag, d) != 0;
-}
-
 // Row helper (j, r): the inter search of MB row r, group by group as the
 // previous frame becomes final over each group's search window (the row
 // coder waits for exactly these), and the deblock of row r, chunk by chunk as
@@ -2791,7 +2769,6 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
   const int nch = db_chunks(a);
   volatile int* vflag = flag;
   DbState st{0, 0, 0, 8};
-  int ahead = 2;  // kHelperFill: group g's first older reference not yet searched ahead (> nref: all)
   for (int g = 0; g < a.ng; g++) {
     trace(tr, 1, g);
     trace(tr, 2, (int)a.epoch * 1000 + r);
@@ -2802,27 +2779,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     // progress word, tagged epoch-2, also covers frame index-3: that frame's
     // row r+2 waited for index-3's row r+4 over a wider window), so these
     // searches fill what used to be the wait for the previous frame.
-    if (kHelperFill && a.inter && a.nref >= 2) {
-      // Group g's older references not yet searched (during group g-1's
-      // wait), then group g+1's while the previous frame is not final over
-      // group g's window, one at a time: a state machine over (group cur,
-      // reference off) with one search site (inlined once).
-      const uint64_t ts = acct_now();
-      int cur = g, off = ahead;
-      if (off > a.nref) cur = g + 1, off = 2;
-      for (;;) {
-        if (cur != g && (cur >= a.ng || off > a.nref || prev_ready(a, r, g, flag))) break;
-        if (off == 2) {  // a group's first older search: its source, frame index-2's window, zero-MV
-          group_source(a, r, cur, L.inter);
-          helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, cur, 1), L.db, st, flag);
-          zero_mv_older(a, r, cur, L.inter);
-        }
-        inter_task(a, r, cur, off, L.inter, L.db, st, flag, cur == g ? is : nullptr, 0);
-        if (++off > a.nref && cur == g) cur = g + 1, off = 2;
-      }
-      ahead = cur == g + 1 ? off : 2;  // group g+1's first reference left to search
-      acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
-    } else if (kGroupSource && a.inter) {
+    if (kGroupSource && a.inter) {
       if (!kHelperSrcDma) {
         group_source(a, r, g, L.inter);
       } else {
@@ -2835,7 +2792,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
         if (g + 1 < a.ng) group_source(a, r, g + 1, L.inter, true);
       }
     }
-    if (!kHelperFill && a.inter && a.nref >= 2) {
+    if (a.inter && a.nref >= 2) {
       helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag,
                   kSpecStage ? &L.inter.full : nullptr, inter_need_cols(a, g, 2));
       const uint64_t ts = acct_now();
