@@ -1600,9 +1600,13 @@ __device__ __forceinline__ int db_chunks(const FA& a) { return (a.wa + (1 << a.d
 #ifndef CAIRO_ABOVE_BATCH
 #define CAIRO_ABOVE_BATCH 1
 #endif
-// The filters of a 64-column chunk over all four waves (1) or in wave 0 (0).
+// The filters of a 64-column chunk over all four waves (1: a workgroup
+// barrier between the four phases) or in wave 0 (0: its LDS operations run in
+// order, no barriers; the other waves go on to the write-out's barrier).
+// Round 4, 4K: 0 is +0.3 % over five alternating rounds
+// (profiles/r04/ab_4k_s.txt, ab_4k_t.txt).
 #ifndef CAIRO_DB_SPREAD
-#define CAIRO_DB_SPREAD 1
+#define CAIRO_DB_SPREAD 0
 #endif
 constexpr bool kDbSpread = CAIRO_DB_SPREAD;
 constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
