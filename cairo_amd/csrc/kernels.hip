@@ -1929,7 +1929,16 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
 // Columns are circular (x & 127, chroma x & 63); the first 16 (4) columns are
 // repeated after the last so that a row read never wraps.  Pitches: 74 / 37
 // dwords, so the 16 rows a candidate group reads hit 16 distinct banks.
-constexpr int kCwLP = 148;  // luma pitch (elements): 128 + 16-column tail + pad
+// Luma pitch (elements): 128 + 16-column tail + pad.  Only 2- and 4-byte
+// accesses touch this window, so the pitch is free: an odd number of dwords
+// (150 elements = 75) puts the 16 rows of a candidate's lane group on 16
+// distinct banks of either parity, so the wave's other groups (offsets of a
+// search step) do not all land on the same 16 even banks (148 = 74 dwords).
+#ifndef CAIRO_CW_PITCH
+#define CAIRO_CW_PITCH 150
+#endif
+constexpr int kCwLP = CAIRO_CW_PITCH;
+static_assert(kCwLP % 2 == 0 && kCwLP >= 144, "coder window rows: dword pairs, 128 + 16-column tail");
 constexpr int kCwCP = 74;   // chroma pitch: 64 + 4-column tail + pad
 constexpr int kLumaTail = 16, kChromaTail = 4;
 
