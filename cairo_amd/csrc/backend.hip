@@ -45,14 +45,15 @@ constexpr int kMaxStages = 256;
 constexpr int kLaunchSlots = 64;    // per-launch host records (frame views, timing events), reused round-robin
 constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engine
 // Frames per launch by default, from measured sweeps (DESIGN.md §4.2,
-// tools/batch_sweep.sh).  With the pools shared between consecutive launches
+// tools/sweep_bench.sh).  With the pools shared between consecutive launches
 // (k_engine next_task) a batch's tail no longer idles half the workers, so
 // larger batches pay: 32 up to about 1080p (1080p: 2981 at 12, 3460 at 24,
-// 3551 at 32 Mpix/s), 28 above (final engine, 4K: 4222 at 20, 4389-4413 at
-// 24, 4443-4454 at 28, 4235 at 32).
-constexpr int kMidFrameMBs = 16000;
+// 3551 at 32 Mpix/s); at 4K 28 was best in round 3 (4443-4454 vs 4235 at
+// 32), and on the round-4 engine 32 is (5838 vs 5808 Mpix/s, three
+// alternating rounds, profiles/r04/batch_ab_4k.txt).
 inline int default_batch(size_t mbs) {
-  return mbs <= (size_t)kMidFrameMBs ? 32 : 28;
+  (void)mbs;
+  return 32;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 // The output_cache slots are allocated in chunks of at most this size, each
