@@ -43,7 +43,7 @@ PEER_SIZE = 3 * 4 + 7 * 4 + 2 * 8 + MAX_COEF_CHUNKS * 8 + 2 * 64 + MAX_COEF_CHUN
 # EVX_PEEK_STATE (reference evx1.h:55-64)
 PEEK_SOURCE, PEEK_PREDICTION, PEEK_BLOCK_TABLE, PEEK_QUANT_TABLE, PEEK_SPMP_TABLE, PEEK_BLOCK_VARIANCE, \
     PEEK_DESTINATION = range(7)
-MAX_BATCH = 32  # kMaxBatch (kernels.h): frames per engine launch, stamp layout
+MAX_BATCH = 48  # kMaxBatch (kernels.h CAIRO_MAX_BATCH): frames per engine launch, stamp layout
 EVX_ERROR_HARDWAREFAIL = 5
 
 

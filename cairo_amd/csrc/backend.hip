@@ -49,11 +49,13 @@ constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engi
 // (k_engine next_task) a batch's tail no longer idles half the workers, so
 // larger batches pay: 32 up to about 1080p (1080p: 2981 at 12, 3460 at 24,
 // 3551 at 32 Mpix/s); at 4K 28 was best in round 3 (4443-4454 vs 4235 at
-// 32), and on the round-4 engine 32 is (5838 vs 5808 Mpix/s, three
-// alternating rounds, profiles/r04/batch_ab_4k.txt).
+// 32); on the round-4 engine larger launches pay there: 32 over 28 (5838 vs
+// 5808 Mpix/s, three alternating rounds, profiles/r04/batch_ab_4k.txt), and
+// with the cap raised to 48: 32 / 36 / 40 / 44 -> 5820 / 5828 / 5856 / 5868
+// (two rounds, profiles/r04/batch_cap_4k.txt).
+constexpr int kMidFrameMBs = 16000;
 inline int default_batch(size_t mbs) {
-  (void)mbs;
-  return 32;
+  return mbs <= (size_t)kMidFrameMBs ? 32 : 40;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 // The output_cache slots are allocated in chunks of at most this size, each

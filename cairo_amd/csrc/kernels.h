@@ -127,7 +127,7 @@ struct Acct {
 
 // Frames per engine launch.
 #ifndef CAIRO_MAX_BATCH
-#define CAIRO_MAX_BATCH 32
+#define CAIRO_MAX_BATCH 48
 #endif
 constexpr int kMaxBatch = CAIRO_MAX_BATCH;
 // Members of a frame-interleaved group (cairo_ctx_join_group).

@@ -88,14 +88,14 @@ def test_task_order_rejects_bad_sizes(cairo):
     with pytest.raises(cairo.CairoError):
         cairo.task_order(0, 1)
     with pytest.raises(cairo.CairoError):
-        cairo.task_order(10, 33)
+        cairo.task_order(10, 49)
 
 
 @pytest.mark.parametrize("hmb", [3, 18, 45, 68, 99, 100, 135, 270])
 def test_label_queues_partition_the_order(cairo, hmb):
     """XCD-banded queues (kernels.h kLabels): each label's queue is the
     launch's task order restricted to that label's rows, a contiguous band."""
-    for frames in (1, 2, 7, 28, 32):
+    for frames in (1, 2, 7, 28, 32, 40, 48):
         o, slope = cairo.task_order(hmb, frames)
         q, seg, nlab = cairo.task_queues(hmb, frames)
         assert nlab == (8 if hmb >= 100 else 1)
