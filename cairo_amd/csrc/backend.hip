@@ -52,10 +52,13 @@ constexpr int kTimed = 3;        // timed kernels: convert, (inter: fused), engi
 // 32); on the round-4 engine larger launches pay there: 32 over 28 (5838 vs
 // 5808 Mpix/s, three alternating rounds, profiles/r04/batch_ab_4k.txt), and
 // with the cap raised to 48: 32 / 36 / 40 / 44 -> 5820 / 5828 / 5856 / 5868
-// (two rounds, profiles/r04/batch_cap_4k.txt).
-constexpr int kMidFrameMBs = 16000;
+// (two rounds, profiles/r04/batch_cap_4k.txt).  But two 40-frame launches
+// in flight leave only 16 of the default 96 staging slots to the host entropy
+// pipeline: end to end fell to 82 % of the hot path (profiles/r04/
+// bench_4k_batch40.json), so the default stays at 32 everywhere.
 inline int default_batch(size_t mbs) {
-  return mbs <= (size_t)kMidFrameMBs ? 32 : 40;
+  (void)mbs;
+  return 32;
 }
 constexpr int kSyncAreas = 3;    // launch b uses area b % 3; launch b+1 reads it too
 // The output_cache slots are allocated in chunks of at most this size, each

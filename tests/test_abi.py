@@ -57,7 +57,7 @@ def test_default_batch(cairo):
     assert cairo.default_batch(352, 288) == 32
     assert cairo.default_batch(1280, 720) == 32
     assert cairo.default_batch(1920, 1080) == 32
-    assert cairo.default_batch(3840, 2160) == 40
+    assert cairo.default_batch(3840, 2160) == 32
     assert cairo.default_batch(0, 720) == 0
 
 

@@ -46,11 +46,11 @@ def test_timed_1080p_default_batch(orc, cairo):
 
 
 def test_timed_4k_default_batch(orc, cairo):
-    """configs[3] on one GPU: 4K q=16 R=4, default 40 frames per launch with
-    helper priority, 43 frames: two overlapping launches, 3 live references;
+    """configs[3] on one GPU: 4K q=16 R=4, default 32 frames per launch with
+    helper priority, 35 frames: two overlapping launches, 3 live references;
     feed outputs (bench.py's timed mode), payloads checked."""
-    assert cairo.default_batch(3840, 2160) == 40
-    _run_batched(orc, cairo, 3840, 2160, 4, 16, 43, 0, outputs=cairo.OUT_FEED)
+    assert cairo.default_batch(3840, 2160) == 32
+    _run_batched(orc, cairo, 3840, 2160, 4, 16, 35, 0, outputs=cairo.OUT_FEED)
 
 
 def test_timed_4k_many_launches(orc, cairo):
@@ -70,7 +70,7 @@ def test_timed_4k_both_outputs(orc, cairo):
     _run_batched(orc, cairo, 3840, 2160, 4, 16, 6, 0, outputs=cairo.OUT_FEED | cairo.OUT_COEF)
 
 
-@pytest.mark.parametrize("q,frames", [(1, 43), (8, 43), (31, 43)])
+@pytest.mark.parametrize("q,frames", [(1, 35), (8, 35), (31, 35)])
 def test_4k_quality_sweep(orc, cairo, q, frames):
     """configs[4]: the 4K quality sweep (VAQ on), default launch, feed
     outputs.  q = 1 and 31 (the ends of the sweep) and 8 over 31 frames: two
