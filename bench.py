@@ -386,7 +386,10 @@ def main():
     e2e_records = {}
     if not a.no_end_to_end:
         note(rank, "end-to-end leg")
-        ctx2 = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
+        # the pipeline's depth: two launches in flight hold 2 * batch staging
+        # slots, the host entropy works on the rest; 128 (not the library's
+        # 96) keeps 64 for it at 32 frames per launch
+        ctx2 = share(cairo_amd.Context(w, h, ring, device=local, stages=a.stages or E2E_STAGES))
         ctx2.set_batch(batch)
         # twice the timed leg's frames (the resident ones, cycled), so that the
         # last launch's entropy tail weighs half as much
@@ -595,6 +598,9 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
         out["bit_exact"] = {"frames_checked": n_check, "members_covered": min(world, n_check),
                             "mismatched_frames": mism, "bit_exact": not mism}
     return out
+
+
+E2E_STAGES = 128  # staging slots of the end-to-end leg's context
 
 
 def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier, dist, dev, world, n_check,
