@@ -6,22 +6,30 @@ ring R = 4 (3 inter references), quality 16, band4 synthetic content
 (seed 1234).  --config 720p / 1080p run configs[1] / configs[2].
 
 A step = one engine launch's batch of P-frames (the library's default frames
-per launch for the frame size: 28 at 4K, 32 at 1080p and 720p) through the
-hot path: RGB->YUV, inter search, the macroblock wavefront (intra search,
-classify, transform, VAQ, quantize, reconstruct, in-loop deblock), the
-entropy precode, and each frame's block table + feed bits handed to host
-memory for the arithmetic coder.  --steps 20 therefore times 560 4K frames.  All input frames are
-resident in HBM before the timed region.
+per launch: 32 at every bench size) through the hot path: RGB->YUV, inter
+search, the macroblock wavefront (intra search, classify, transform, VAQ,
+quantize, reconstruct, in-loop deblock), the entropy precode, and each
+frame's block table + feed bits handed to host memory for the arithmetic
+coder.  --steps 20 therefore times 640 frames after 96 warm-up frames.  All
+input frames are resident in HBM before the timed region.  --content noise
+/ static run SURVEY.md §8(d)'s stress and best cases instead of band4.
+
+Every frame is verified (bit_exact in the line): each frame's GPU-precoded
+feed is copied out of its staging slot as it is retired (the only checking
+work inside the timed region), and after timing it is arithmetic-coded on
+host threads into the frame's stream record, whose FNV-1a-64 is compared with
+tests/golden/stream_<config>_q<q>_r<R>.json (the oracle's per-frame record
+hashes of the same band4 stream, made by tests/golden/make_stream_golden.py).
+The end-to-end leg's payloads are checked the same way.
 
 Other legs (rank 0, N = 1), outside the timed region:
-  bit_exact   the first frames of the timed context itself (same launches,
-              same batch) and of the end-to-end pipeline, serialized and
-              compared frame by frame with the oracle (test infrastructure)
   end_to_end  hot path + host entropy on native worker threads (cairo_stream)
   api_encode  evx1_encoder::encode() through the drop-in C++ API, called by a
               C++ program built against include/evx1.h (one frame per call,
               host RGB in, bitstream out: the reference's own interface)
-  cpu_baseline  the oracle (C restatement) on one host core, bounded sample
+  cpu_baseline  the oracle (C restatement) on one host core over a bounded
+              sample; the same frames re-check the golden file's prefix and,
+              for content without a golden (noise, static), the GPU records
 
 Multi-GPU: one process per GPU (torch.distributed.run).  value (N > 1): ONE
 stream over all ranks (BASELINE.json configs[3]: one 4K stream over the
@@ -90,7 +98,152 @@ def parse():
                    help="write the timed engine launches' [start, end) intervals (CSV, ms) to this path")
     p.add_argument("--no-host-rgb", action="store_true", help="skip the pipelined host-RGB (PCIe-inclusive) leg")
     p.add_argument("--host-rgb-steps", type=int, default=12, help="timed steps of the host-RGB leg")
+    p.add_argument("--content", default="band4", choices=["band4", "noise", "static"],
+                   help="band4 (SURVEY.md §8(d) default), noise (no copy blocks, full searches everywhere: the stress "
+                        "case) or static (band4 frame 0 repeated: the best case)")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the per-frame check of every timed frame (no feed copies in the timed region)")
     return p.parse_args()
+
+
+# Frames of one content kind resident in HBM: band4 is a distinct frame per
+# index (the golden stream); noise cycles a pool of distinct random frames
+# (consecutive frames stay uncorrelated); static is one frame.
+NOISE_POOL = 64
+
+
+def content_frame(kind: str, w: int, h: int, t: int) -> np.ndarray:
+    """Source frame t of the bench's stream (RGB888)."""
+    import cairo_amd
+
+    if kind == "band4":
+        return cairo_amd.make_band4(w, h, t)
+    if kind == "static":
+        return cairo_amd.make_band4(w, h, 0)
+    rng = np.random.default_rng(7 * 1000003 + t % NOISE_POOL)  # tests/content.py "noise"
+    return rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+
+
+def content_pool(kind: str, frames: int) -> int:
+    """Distinct resident frames needed for a stream of `frames` frames."""
+    return {"band4": frames, "noise": min(frames, NOISE_POOL), "static": 1}[kind]
+
+
+class Arena:
+    """Append-only host store for per-frame bytes (feeds, payloads): large
+    chunks, pre-touched before the timed region, so retiring a frame costs
+    one memcpy and no allocation."""
+
+    def __init__(self, chunk: int = 256 << 20):
+        self.chunk = chunk
+        self.chunks = []
+        self.cur, self.pos = -1, 0
+
+    def _new(self, size: int) -> None:
+        c = np.empty(size, np.uint8)
+        c.fill(0)  # touch every page now, not at the first copy
+        self.chunks.append(c)
+
+    def grow(self, nbytes: int) -> None:
+        """Pre-touch chunks until about nbytes more fit."""
+        free = (self.chunks[self.cur].size - self.pos if self.cur >= 0 else 0) + \
+            sum(c.size for c in self.chunks[self.cur + 1:])
+        while free < nbytes:
+            self._new(self.chunk)
+            free += self.chunk
+
+    def reserve(self, nbytes: int):
+        """-> (chunk array, byte offset) of nbytes of room (16-byte aligned)."""
+        while self.cur < 0 or self.pos + nbytes > self.chunks[self.cur].size:
+            if self.cur + 1 == len(self.chunks):
+                self._new(max(self.chunk, nbytes))
+            self.cur, self.pos = self.cur + 1, 0
+        off = self.pos
+        self.pos = (off + nbytes + 15) & ~15
+        return self.chunks[self.cur], off
+
+
+class FrameStore:
+    """Every frame a leg encodes, kept for the post-timing check: the
+    GPU-precoded feed (copied out of the staging slot at retire) or, for the
+    end-to-end leg, the payload; a frame whose feed overflowed is coded on
+    the spot from its planes (rare: 4K noise at q=1)."""
+
+    def __init__(self):
+        self.arena = Arena()
+        self.items = {}  # frame -> ("feed" | "pay", chunk, offset, bits) or ("bytes", data, bits)
+        self.max_bytes = 0
+
+    def keep_feed(self, cairo_amd, ctx, f, out, ticket):
+        if out.feed_status == cairo_amd.FEED_VALID:
+            src = out.feed.view(np.uint8)
+            buf, off = self.arena.reserve(src.size)
+            buf[off:off + src.size] = src
+            self.items[f] = ("feed", buf, off, out.feed_bits)
+            self.max_bytes = max(self.max_bytes, src.size)
+        else:
+            self.items[f] = ("bytes",) + payload(cairo_amd, ctx, out, ticket)
+
+    def keep_payload(self, st, f, tk):
+        nb = st.payload_bits(tk)
+        buf, off = self.arena.reserve(nb // 8 + 8)
+        st.collect(tk, buf[off:], 0)
+        self.items[f] = ("pay", buf, off, nb)
+        self.max_bytes = max(self.max_bytes, nb // 8 + 8)
+
+    def reserve_for(self, frames: int) -> None:
+        """Pre-touch room for `frames` more frames of the size seen so far."""
+        if self.max_bytes:
+            self.arena.grow(int(self.max_bytes * 1.25 + 64) * frames)
+
+    def payload(self, cairo_amd, f):
+        it = self.items[f]
+        if it[0] == "bytes":
+            return it[1], it[2]
+        kind, buf, off, nb = it
+        if kind == "feed":
+            words = buf[off:off + (nb + 31) // 32 * 4].view(np.uint32)
+            return cairo_amd.serialize_feed(words, nb)
+        return buf[off:off + (nb + 7) // 8].tobytes(), nb
+
+
+def frame_hashes(cairo_amd, store: FrameStore, w, h, ring, q, threads: int) -> dict:
+    """{frame: FNV-1a-64 hex of the canonical stream record} for every frame in
+    the store, as tests/golden/make_stream_golden.py hashes the oracle's (the
+    arithmetic coding of the feeds runs on `threads` host threads; checker
+    code, after the timed region)."""
+    from oracle import oracle as orc
+
+    def one(f):
+        data, nb = record(cairo_amd, w, h, ring, q, f, *store.payload(cairo_amd, f))
+        return f, f"{orc.fnv1a64(orc.canonical_frame_bytes(data, nb, f == 0)):016x}"
+
+    with ThreadPoolExecutor(max(1, threads)) as pool:
+        return dict(pool.map(one, sorted(store.items)))
+
+
+def golden_stream(config: str, content: str, q: int, ring: int):
+    """The oracle's per-frame record hashes of this stream, or None."""
+    if content != "band4":
+        return None
+    path = os.path.join(ROOT, "tests", "golden", f"stream_{config}_q{q}_r{ring}.json")
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    g["path"] = os.path.relpath(path, ROOT)
+    return g
+
+
+def check_hashes(hashes: dict, golden, frames, timed_from: int) -> dict:
+    """Compare {frame: hash} for `frames` against the golden file."""
+    frames = list(frames)
+    have = golden["frame_fnv1a64"] if golden else []
+    checked = [f for f in frames if f < len(have)]
+    mism = [f for f in checked if hashes.get(f) != have[f]]
+    return {"frames": len(frames), "frames_checked": len(checked),
+            "timed_frames_checked": sum(1 for f in checked if f >= timed_from),
+            "unchecked_frames": len(frames) - len(checked), "mismatched_frames": mism[:50],
+            "mismatches": len(mism)}
 
 
 def algorithmic_bytes(w, h, ring):
@@ -264,20 +417,25 @@ def main():
     batch = a.batch or cairo_amd.default_batch(w, h)
     warm_frames, timed_frames = a.warmup * batch, a.steps * batch
     nframes = warm_frames + timed_frames
+    # the end-to-end leg encodes twice the timed frames after the same warm-up:
+    # every frame of every leg is a distinct resident frame of one stream, the
+    # one the golden hashes describe (4K: 1376 frames, 34 GB of HBM)
+    stream_frames = warm_frames + (timed_frames if a.no_end_to_end else 2 * timed_frames)
+    pool_n = content_pool(a.content, max(nframes, stream_frames))
     # synthetic input, generated on host threads and uploaded to HBM before timing
-    frames = torch.empty((nframes, h, w, 3), dtype=torch.uint8, device=torch.device("cuda", local))
+    frames = torch.empty((pool_n, h, w, 3), dtype=torch.uint8, device=torch.device("cuda", local))
     chunk = 16
     with ThreadPoolExecutor(max(1, min(8, host_cpus()))) as pool:
-        for c0 in range(0, nframes, chunk):
-            n = min(chunk, nframes - c0)
-            host = np.stack(list(pool.map(lambda f: cairo_amd.make_band4(w, h, f), range(c0, c0 + n))))
+        for c0 in range(0, pool_n, chunk):
+            n = min(chunk, pool_n - c0)
+            host = np.stack(list(pool.map(lambda f: content_frame(a.content, w, h, f), range(c0, c0 + n))))
             frames[c0:c0 + n].copy_(torch.from_numpy(host))
     torch.cuda.synchronize()
     base, stride = frames.data_ptr(), w * h * 3
-    note(rank, f"{nframes} {w}x{h} frames resident in HBM")
+    note(rank, f"{pool_n} {w}x{h} {a.content} frames resident in HBM")
 
     def frame_ptr(f):
-        return base + f * stride
+        return base + (f % pool_n) * stride
 
     ctx = share(cairo_amd.Context(w, h, ring, device=local, **({"stages": a.stages} if a.stages else {})))
     ctx.set_batch(batch)
@@ -294,29 +452,31 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # the frames the bit-exact check compares (rank 0, N = 1: the oracle's sample)
+    # the oracle's live sample (rank 0, N = 1): the CPU baseline's frames;
+    # without a golden file (noise, static) also every frame of the first
+    # launch and the head of the second
     check = rank == 0 and world == 1 and not a.no_cpu_baseline
+    golden = golden_stream(a.config, a.content, q, ring)
     # CPU baseline: frame 0 + a bounded sample of P-frames (about 60 Mpixels)
     cpu_pframes = a.cpu_frames or max(2, min(48, int(60e6 / (w * h))))
-    # bit-exact sample: every frame of the first launch and the head of the
-    # second (which overlaps the first and shares its workers), at least 31
-    n_check = max(cpu_pframes + 1, batch + 3, 31) if check else 0
+    n_check = (cpu_pframes + 1 if golden else max(cpu_pframes + 1, batch + 3)) if check else 0
     n_check = min(n_check, warm_frames)
-    hot_records = {}
+    verify = not a.no_verify
+    hot = FrameStore()
 
-    def keep_record(f, out, ticket):
-        if f < n_check:
-            hot_records[f] = record(cairo_amd, w, h, ring, q, f, *payload(cairo_amd, ctx, out, ticket))
+    def keep(f, out, ticket):
+        hot.keep_feed(cairo_amd, ctx, f, out, ticket)
 
     # warmup: frame 0 (I) + P-frames, in the same context and launches as the timed region
-    run_hot_path(ctx, frame_ptr, 0, warm_frames, q, stages, keep_record)
+    run_hot_path(ctx, frame_ptr, 0, warm_frames, q, stages, keep if verify or n_check else None)
     ctx.sync()
+    hot.reserve_for(timed_frames)
     note(rank, "warm-up done")
     ctx.set_profiling(True)
     ctx.take_timings()
     barrier()
     t0 = time.perf_counter()
-    run_hot_path(ctx, frame_ptr, warm_frames, timed_frames, q, stages)
+    run_hot_path(ctx, frame_ptr, warm_frames, timed_frames, q, stages, keep if verify else None)
     ctx.sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -383,7 +543,7 @@ def main():
                             "on band4) / engine busy time; peak = packed 16-bit VALU rate (2 pixel-ops per lane)"}
 
     e2e = None
-    e2e_records = {}
+    e2e_store = FrameStore() if verify else None
     if not a.no_end_to_end:
         note(rank, "end-to-end leg")
         # the pipeline's depth: two launches in flight hold 2 * batch staging
@@ -391,10 +551,10 @@ def main():
         # 96) keeps 64 for it at 32 frames per launch
         ctx2 = share(cairo_amd.Context(w, h, ring, device=local, stages=a.stages or E2E_STAGES))
         ctx2.set_batch(batch)
-        # twice the timed leg's frames (the resident ones, cycled), so that the
-        # last launch's entropy tail weighs half as much
-        e2e = end_to_end(cairo_amd, ctx2, lambda f: frame_ptr(f % nframes), a, ring, q, w, h, warm_frames,
-                         2 * timed_frames, barrier, dist, dev, world, n_check, e2e_records, batch)
+        # twice the timed leg's frames (all resident, the same stream), so
+        # that the last launch's entropy tail weighs half as much
+        e2e = end_to_end(cairo_amd, ctx2, frame_ptr, a, ring, q, w, h, warm_frames,
+                         2 * timed_frames, barrier, dist, dev, world, e2e_store, batch)
         ctx2.close()
     ctx.close()
     host_leg = None
@@ -432,8 +592,14 @@ def main():
         # below name their denominators
         "vs_baseline": None,
         "dtype": "int16",
-        "data": "synthetic (band4 generator, seed 1234; SURVEY.md §8(d)), resident in HBM",
-        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}] {where})",
+        "data": {"band4": "synthetic (band4 generator, seed 1234; SURVEY.md §8(d)), resident in HBM",
+                 "noise": f"synthetic uniform RGB noise ({NOISE_POOL} distinct frames cycled; SURVEY.md §8(d) "
+                          f"stress case: no copy blocks), resident in HBM",
+                 "static": "synthetic static scene (band4 frame 0 repeated; SURVEY.md §8(d) best case), resident "
+                           "in HBM"}[a.content],
+        "content": a.content,
+        "config": {"workload": f"{w}x{h} p-frame q={q} ring R={ring} (BASELINE.json configs[{cfg_idx}] {where})"
+                               + ("" if a.content == "band4" else f", {a.content} content"),
                    "width": w, "height": h, "ring": ring, "quality": q, "frames_per_step": batch,
                    "timed_frames": timed_frames, "ms_per_frame": round(head["ms_per_step"] / batch, 4),
                    "parallelism": "one stream on one GPU" if world == 1 else
@@ -446,12 +612,48 @@ def main():
         "api_encode": api,
         "single_stream": single,
     }
+    exact = None
+    if verify or n_check:
+        note(rank, "checking every frame")
+        tv = time.perf_counter()
+        threads = max(1, host_cpus() // world)
+        hot_h = frame_hashes(cairo_amd, hot, w, h, ring, q, threads)
+        e2e_h = frame_hashes(cairo_amd, e2e_store, w, h, ring, q, threads) if e2e_store and e2e_store.items else {}
+        del hot, e2e_store
+        exact = {"golden": ({"path": golden["path"], "frames": golden["frames"]} if golden else None)}
+        if verify:
+            exact["hot_path_context"] = check_hashes(hot_h, golden, range(nframes), warm_frames)
+            if e2e_h:
+                exact["end_to_end_pipeline"] = check_hashes(e2e_h, golden, range(stream_frames), warm_frames)
+        exact["check_s"] = round(time.perf_counter() - tv, 2)
     if check:
-        note(rank, "CPU baseline and bit-exact check")
-        result["cpu_baseline"], result["bit_exact"] = cpu_baseline(cairo_amd, w, h, ring, q, cpu_pframes, n_check - 1,
-                                                                   hot_records, e2e_records, batch)
+        note(rank, "CPU baseline and the oracle's live sample")
+        result["cpu_baseline"], sample = cpu_baseline(cairo_amd, a.content, w, h, ring, q, cpu_pframes, n_check - 1,
+                                                      hot_h, e2e_h, golden, batch)
+        exact["oracle_sample"] = sample
     else:
         result["cpu_baseline"] = None
+    if exact is not None:
+        hp = exact.get("hot_path_context", {})
+        bad = sum(exact.get(k, {}).get("mismatches", 0) for k in ("hot_path_context", "end_to_end_pipeline"))
+        bad += len(exact.get("oracle_sample", {}).get("mismatched_frames", []))
+        exact["frames_checked"] = hp.get("timed_frames_checked", 0)  # timed frames, against the golden hashes
+        exact["timed_frames"] = timed_frames
+        exact["mismatches"] = bad
+        exact["bit_exact"] = bad == 0 and bool(exact["frames_checked"] == timed_frames or
+                                               ("oracle_sample" in exact and not golden))
+        exact["what"] = ("every frame of the timed context (warm-up and timed, same launches) and of the end-to-end "
+                         "pipeline: the GPU feed / payload arithmetic-coded on host threads after the timed region, "
+                         "the frame's stream record hashed (FNV-1a-64, header byte 7 and tail bits masked) and "
+                         "compared with the oracle's hashes of the same stream (golden); oracle_sample re-encodes "
+                         "the first frames live on this host")
+    if world > 1:
+        allx = [None] * world
+        dist.all_gather_object(allx, exact)
+        exact = {"ranks": allx, "bit_exact": all(x and x.get("bit_exact") for x in allx),
+                 "frames_checked": sum((x or {}).get("frames_checked", 0) for x in allx),
+                 "what": "every rank's own replica stream, every frame, against the golden hashes"}
+    result["bit_exact"] = exact
     vs = {}
     if a.config in REF_CPU_MPIX:
         vs["survey_xeon_reference"] = round(result["value"] / REF_CPU_MPIX[a.config], 1)
@@ -509,14 +711,16 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
     def step(what, fn):
         return agreed_step(dist, gloo, rank, state, what, fn)
 
+    store = FrameStore()
+
     def run(first, count, keep):
         inflight = deque()
 
         def retire():
             n, t = inflight.popleft()
             out = ctx.wait(t, copy=False)
-            if keep and n < n_check:
-                recs[n] = record(cairo_amd, w, h, ring, q, n, *payload(cairo_amd, ctx, out, t))
+            if keep:
+                store.keep_feed(cairo_amd, ctx, n, out, t)
             ctx.release(t)
 
         for n in range(first, first + count):
@@ -551,15 +755,27 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
         note(rank, "single stream: group joined")
     if step("warm-up", lambda: run(0, warm, True)):
         note(rank, "single stream: warm-up done")
+    store.reserve_for(len(range(rank, timed, world)))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if step("timed", lambda: run(warm, timed, False)):
+    if step("timed", lambda: run(warm, timed, not a.no_verify)):
         res = time.perf_counter() - t0
         note(rank, "single stream: timed run done")
     err = state["err"]
-    mine = len(range(rank, timed, world))  # this member's frames of the timed region
+    # this member's frames, checked after the timed region: the live oracle's
+    # first frames on rank 0 below, every frame against the golden hashes
+    mine = {}
+    if not err:
+        mine = frame_hashes(cairo_amd, store, w, h, ring, q, max(1, host_cpus() // world))
+    del store
+    golden = golden_stream(a.config, a.content, q, ring)
+    gcheck = check_hashes(mine, golden, sorted(mine), warm) if golden else None
+    recs = {n: mine[n] for n in mine if n < n_check}
+    own = len(range(rank, timed, world))  # this member's frames of the timed region
     per_member = [None] * world
-    dist.all_gather_object(per_member, round(res * 1e3 / max(mine, 1), 4) if res else None, group=gloo)
+    dist.all_gather_object(per_member, round(res * 1e3 / max(own, 1), 4) if res else None, group=gloo)
+    gchecks = [None] * world
+    dist.all_gather_object(gchecks, gcheck, group=gloo)
     ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=gloo)
     elt = torch.tensor([res or 0.0], dtype=torch.float64)
@@ -591,23 +807,30 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
         e.set_quality(q)
         mism = []
         for t in range(n_check):
-            data, nb = e.encode(cairo_amd.make_band4(w, h, t))
-            if t not in got or orc.canonical_frame_bytes(got[t][0], got[t][1], t == 0) != \
-                    orc.canonical_frame_bytes(data, nb, t == 0):
+            data, nb = e.encode(content_frame(a.content, w, h, t))
+            if got.get(t) != f"{orc.fnv1a64(orc.canonical_frame_bytes(data, nb, t == 0)):016x}":
                 mism.append(t)
-        out["bit_exact"] = {"frames_checked": n_check, "members_covered": min(world, n_check),
-                            "mismatched_frames": mism, "bit_exact": not mism}
+        ex = {"oracle_sample": {"frames": n_check, "members_covered": min(world, n_check), "mismatched_frames": mism}}
+        bad = len(mism)
+        if all(gchecks):
+            ex["members_vs_golden"] = gchecks
+            ex["frames_checked"] = sum(g["timed_frames_checked"] for g in gchecks)
+            bad += sum(g["mismatches"] for g in gchecks)
+        ex["mismatches"] = bad
+        ex["bit_exact"] = bad == 0 and (ex.get("frames_checked") == timed or a.no_verify or not all(gchecks))
+        out["bit_exact"] = ex
     return out
 
 
 E2E_STAGES = 128  # staging slots of the end-to-end leg's context
 
 
-def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier, dist, dev, world, n_check,
-               records, batch=0):
+def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier, dist, dev, world, store,
+               batch=0):
     """Hot path + host entropy through the native frame pipeline
     (cairo_stream_*: entropy on a pool of C++ worker threads); every frame's
-    payload is appended to one output buffer (bitstream produced)."""
+    payload is collected into host memory (store: kept for the post-timing
+    check; without one, into one reused buffer)."""
     stages = ctx.stages
     if a.entropy_threads <= 0:
         a.entropy_threads = max(1, min(14, host_cpus() // world - 2))
@@ -616,9 +839,8 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier
     tl = []
 
     def collect(f, tk):
-        if f < n_check:
-            data, nbits = st.collect(tk)
-            records[f] = record(cairo_amd, w, h, ring, q, f, data, nbits)
+        if store is not None:
+            store.keep_payload(st, f, tk)
         else:
             st.collect(tk, out, 0)
         tl.append(st.timeline(tk))
@@ -633,6 +855,8 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier
             collect(*inflight.popleft())
 
     run(0, warm)  # I + P warmup
+    if store is not None:
+        store.reserve_for(timed)
     barrier()
     t0 = time.perf_counter()
     tl.clear()
@@ -658,7 +882,7 @@ def end_to_end(cairo_amd, ctx, frame_ptr, a, ring, q, w, h, warm, timed, barrier
         if st_us > 0:
             out["steady_value"] = round(w * h * (timed - batch) * world / st_us, 3)
     out["note"] = ("hot path + host entropy (native frame pipeline, cairo_stream_*); payload bits produced; "
-                   "twice the timed leg's frames (resident frames cycled)")
+                   "twice the timed leg's frames, every one a distinct resident frame of the same stream; each payload kept for the check")
     return out
 
 
@@ -750,13 +974,13 @@ def api_encode(w, h, ring, q, frames):
                     "host entropy on the calling thread)"}
 
 
-def cpu_baseline(cairo_amd, w, h, ring, q, pframes, last, hot_records, e2e_records, batch):
+def cpu_baseline(cairo_amd, content, w, h, ring, q, pframes, last, hot_h, e2e_h, golden, batch):
     """The oracle (plain-C restatement of the reference encoder, test
     infrastructure) on one host core: frame 0 (I) + `pframes` P-frames timed
     (a bounded sample); P-frame Mpix/s.  It then continues, untimed, to frame
-    `last`, and the GPU records of frames 0..last, taken from the timed
-    hot-path context and from the end-to-end pipeline, are compared bit for
-    bit (the checker role)."""
+    `last`; the records of frames 0..last are hashed as the golden file's and
+    compared with the GPU's (timed context, end-to-end pipeline) and with the
+    golden file's prefix (the checker role) -> (baseline, sample check)."""
     from oracle import oracle as orc
 
     e = orc.OracleEncoder(ring)
@@ -765,34 +989,27 @@ def cpu_baseline(cairo_amd, w, h, ring, q, pframes, last, hot_records, e2e_recor
     tp = 0.0
     orc.op_counts(reset=True)
     for t in range(last + 1):
-        rgb = cairo_amd.make_band4(w, h, t)
+        rgb = content_frame(content, w, h, t)
         t0 = time.perf_counter()
         data, n = e.encode(rgb)
         dt = time.perf_counter() - t0
         if 0 < t <= pframes:
             tp += dt
-        ref.append(orc.canonical_frame_bytes(data, n, t == 0))
+        ref.append(f"{orc.fnv1a64(orc.canonical_frame_bytes(data, n, t == 0)):016x}")
     base = {"value": round(w * h * pframes / tp / 1e6, 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
-            "sample": f"{w}x{h} q={q} R={ring}: frame 0 (I, untimed) + {pframes} P-frames timed, band4 seed 1234, "
+            "sample": f"{w}x{h} q={q} R={ring}: frame 0 (I, untimed) + {pframes} P-frames timed, {content} content, "
                       f"oracle/evx_oracle.c -O3 -march=x86-64-v3, one thread",
             "cpu": cpu_model(), "host_cpus_available": host_cpus()}
-
-    def compare(recs):
-        mism = [t for t in range(last + 1)
-                if t not in recs or orc.canonical_frame_bytes(recs[t][0], recs[t][1], t == 0) != ref[t]]
-        return {"frames_checked": last + 1, "launches_covered": -(-(last + 1) // batch), "mismatched_frames": mism}
-
-    hot = compare(hot_records)
-    exact = {"hot_path_context": hot,
-             "what": "frames 0..n of the timed context (same batch, overlapping launches: all of launch 0 and the "
-                     "head of launch 1) serialized on the host from the GPU-precoded feed, and of the end-to-end "
-                     "pipeline, vs the oracle's stream records (header byte 7 and tail bits masked)"}
-    ok = not hot["mismatched_frames"]
-    if e2e_records:
-        exact["end_to_end_pipeline"] = compare(e2e_records)
-        ok = ok and not exact["end_to_end_pipeline"]["mismatched_frames"]
-    exact["bit_exact"] = ok
-    return base, exact
+    frames = range(last + 1)
+    mism = sorted({t for t in frames if hot_h.get(t) != ref[t]} |
+                  ({t for t in frames if e2e_h.get(t) != ref[t]} if e2e_h else set()))
+    sample = {"frames": last + 1, "launches_covered": -(-(last + 1) // batch), "mismatched_frames": mism}
+    if golden:
+        have = golden["frame_fnv1a64"]
+        sample["golden_prefix_matches"] = all(t < len(have) and have[t] == ref[t] for t in frames)
+        if not sample["golden_prefix_matches"]:
+            sample["mismatched_frames"] = sorted(set(mism) | {-1})  # -1: the golden file itself
+    return base, sample
 
 
 if __name__ == "__main__":

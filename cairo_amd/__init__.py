@@ -654,6 +654,12 @@ class Stream:
         self._keep.pop(ticket, None)
         return p.value
 
+    def payload_bits(self, ticket: int) -> int:
+        """The frame's payload length in bits (waits for its entropy stage)."""
+        p = ctypes.c_uint64(0)
+        _ck(self.L.cairo_stream_payload_bits(self.h, ticket, ctypes.byref(p)), "cairo_stream_payload_bits")
+        return p.value
+
     def timeline(self, ticket: int):
         """(submitted, outputs on host, entropy start, entropy end, collected), us."""
         t = (ctypes.c_double * 5)()

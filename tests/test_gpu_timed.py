@@ -1,11 +1,12 @@
 """GPU parity of the configurations bench.py times, and of the drop-in API.
 
 * The pipelined Context with the library's default frames per launch (32 at
-  720p and 1080p, 28 at 4K), several launches in flight on two streams sharing
-  their worker pools and, above 4000 macroblocks, helper issue priority:
-  exactly what bench.py's
-  timed region runs (BASELINE.json configs[1..4]), frame by frame against the
-  oracle (block table, coefficients) and every ring slot at the end.
+  every bench size), several launches in flight on two streams sharing their
+  worker pools and, above 4000 macroblocks, helper issue priority: exactly
+  what bench.py's timed region runs (BASELINE.json configs[1..4]), frame by
+  frame against the oracle (block table, coefficients) and every ring slot at
+  the end; and over 160-200 frames (five or more launches, recycled sync
+  areas) against the oracle's golden stream hashes.
 * evx1_encoder::encode() called from C++ through the vtable
   (tests/api/evx1_api_caller.cpp, built against include/evx1.h), peek() views,
   periodic intra (evx1enc.cpp:143-150), recovery after a reported timeout, the
@@ -57,11 +58,71 @@ def test_timed_4k_many_launches(orc, cairo):
     """configs[3] past the first launches: 4K q=16 R=4 with the bench's
     banded queues, helper priority, feed outputs and device-resident frames,
     10 frames per launch, 44 frames = 5 launches.  Launch b reuses the sync
-    area, task queue and frame views of launch b-3 (backend.hip flush: areas
-    rotate mod 3) while launch b-1 still runs beside it, so launches 3 and 4
-    run on recycled state; every frame's payload bits, block table and
-    coefficients and every ring slot at the end against the oracle."""
+    area and task queue of launch b-3 (backend.hip flush: areas rotate mod 3)
+    while launch b-1 still runs beside it, so launches 3 and 4 run on
+    recycled sync state (the frame views are a 64-slot ring, not recycled
+    here: test_many_launches_queued covers that); every frame's payload bits,
+    block table and coefficients and every ring slot at the end against the
+    oracle."""
     _run_batched(orc, cairo, 3840, 2160, 4, 16, 44, 10, outputs=cairo.OUT_FEED, device_frames=True)
+
+
+def _golden_stream_run(cairo, config, frames, batch=0):
+    """bench.py's timed leg exactly (its run_hot_path, FrameStore and record
+    hashing): `frames` band4 frames resident in HBM, the library's default
+    frames per launch, feed outputs, up to `stages` in flight; every frame's
+    record hash against tests/golden/stream_<config>_*.json (the oracle's, made
+    off-box), so long runs need no oracle time here."""
+    import ctypes
+
+    import bench
+
+    w, h, ring, q, _ = bench.CONFIGS[config]
+    g = bench.golden_stream(config, "band4", q, ring)
+    assert g is not None and g["frames"] >= frames, f"golden stream for {config} has too few frames"
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime the library uses
+    size = w * h * 3
+    dev = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(frames * size)) == 0
+    try:
+        for t in range(frames):
+            f = cairo.make_band4(w, h, t)
+            assert hip.hipMemcpy(ctypes.c_void_p(dev.value + t * size), f.ctypes.data_as(ctypes.c_void_p),
+                                 ctypes.c_size_t(size), 1) == 0
+        ctx = cairo.Context(w, h, ring)
+        ctx.set_outputs(cairo.OUT_FEED)
+        if batch:
+            ctx.set_batch(batch)
+        store = bench.FrameStore()
+        bench.run_hot_path(ctx, lambda t: dev.value + t * size, 0, frames, q, ctx.stages,
+                           lambda t, out, tk: store.keep_feed(cairo, ctx, t, out, tk))
+        ctx.sync()
+        ctx.close()
+    finally:
+        hip.hipFree(dev)
+    got = bench.frame_hashes(cairo, store, w, h, ring, q, threads=8)
+    r = bench.check_hashes(got, g, range(frames), 0)
+    assert r["frames_checked"] == frames
+    assert r["mismatches"] == 0, f"{config}: frames {r['mismatched_frames']} differ from the golden stream"
+
+
+def test_timed_4k_golden_160(cairo):
+    """configs[3] at the bench's default 32 frames per launch over 160
+    frames: five launches, so launches 3 and 4 run on sync areas, task queues
+    and queue counters recycled from launches 0 and 1 (areas rotate mod 3),
+    every frame's payload against the oracle's golden hashes."""
+    assert cairo.default_batch(3840, 2160) == 32
+    _golden_stream_run(cairo, "4k", 160)
+
+
+def test_timed_1080p_golden_160(cairo):
+    """configs[2] (q=8, R=4), 160 frames at 32 per launch, against the golden stream."""
+    _golden_stream_run(cairo, "1080p", 160)
+
+
+def test_timed_720p_golden_200(cairo):
+    """configs[1] (q=16, R=2), 200 frames at 32 per launch, against the golden stream."""
+    _golden_stream_run(cairo, "720p", 200)
 
 
 def test_timed_4k_both_outputs(orc, cairo):
@@ -73,8 +134,8 @@ def test_timed_4k_both_outputs(orc, cairo):
 @pytest.mark.parametrize("q,frames", [(1, 35), (8, 35), (31, 35)])
 def test_4k_quality_sweep(orc, cairo, q, frames):
     """configs[4]: the 4K quality sweep (VAQ on), default launch, feed
-    outputs.  q = 1 and 31 (the ends of the sweep) and 8 over 31 frames: two
-    overlapping 28-frame launches, every payload against the oracle."""
+    outputs.  q = 1 and 31 (the ends of the sweep) and 8 over 35 frames: two
+    overlapping launches (32 + 3 frames), every payload against the oracle."""
     _run_batched(orc, cairo, 3840, 2160, 4, q, frames, 0, outputs=cairo.OUT_FEED)
 
 
