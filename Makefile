@@ -45,7 +45,23 @@ $(API_BIN): tests/api/evx1_api_caller.cpp include/evx1.h include/bitstream.h inc
 $(ORACLE): oracle/evx_oracle.c oracle/evx_oracle.h
 	gcc -O3 -march=x86-64-v3 -std=c11 -fPIC -shared -Wall -o $@ oracle/evx_oracle.c -lm
 
+# Every build switch of the kernels that stays, compiled for gfx950 (no GPU
+# needed): the time-accounting build, the traffic-attribution builds (tools
+# builds only: without CAIRO_TOOLS_BUILD they must be refused), a larger
+# launch cap.
+KNOB_OBJ = build/knobs
+check-knobs:
+	@mkdir -p $(KNOB_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DCAIRO_ACCT=1 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/acct.o
+	$(HIPCC) $(HIPFLAGS) -DCAIRO_TOOLS_BUILD -DCAIRO_ATTR_SKIP=1 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/attr1.o
+	$(HIPCC) $(HIPFLAGS) -DCAIRO_TOOLS_BUILD -DCAIRO_ATTR_SKIP=4 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/attr4.o
+	$(HIPCC) $(HIPFLAGS) -DCAIRO_MAX_BATCH=64 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/batch64.o
+	$(HIPCC) $(HIPFLAGS) -DCAIRO_MAX_BATCH=64 -c $(SRC)/backend.hip -o $(KNOB_OBJ)/batch64_backend.o
+	@if $(HIPCC) $(HIPFLAGS) -DCAIRO_ATTR_SKIP=1 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/refused.o 2>/dev/null; then \
+	  echo "CAIRO_ATTR_SKIP without CAIRO_TOOLS_BUILD was not refused"; exit 1; fi
+	@echo "check-knobs: every build switch compiles; CAIRO_ATTR_SKIP is refused in product builds"
+
 clean:
 	rm -rf build $(LIB) $(ORACLE) $(API_BIN)
 
-.PHONY: all clean
+.PHONY: all clean check-knobs

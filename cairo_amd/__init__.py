@@ -36,6 +36,7 @@ BLOCK_DESC = np.dtype(
 assert BLOCK_DESC.itemsize == 16
 
 EVX_SUCCESS = 0
+API_VERSION = 3  # include/cairo_amd.h CAIRO_AMD_API_VERSION
 OUT_COEF, OUT_FEED = 1, 2  # cairo_ctx_set_outputs
 FEED_NONE, FEED_VALID, FEED_OVERFLOW = 0, 1, 2
 MAX_COEF_CHUNKS = 16  # CAIRO_MAX_COEF_CHUNKS
@@ -147,12 +148,16 @@ def lib() -> ctypes.CDLL:
         "cairo_ctx_decode_frame": (I, [P, P, P, U, P]),
         "cairo_make_band4": (V, [P, U, U, U, U]),
         "cairo_version": (ctypes.c_char_p, []),
+        "cairo_api_version": (I, []),
         "cairo_device_count": (I, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.cairo_api_version() != API_VERSION:
+        raise ImportError(f"{LIB_PATH} has C ABI version {L.cairo_api_version()}, these bindings expect "
+                          f"{API_VERSION} (include/cairo_amd.h CAIRO_AMD_API_VERSION): rebuild with `make`")
     _lib = L
     return L
 

@@ -145,7 +145,6 @@ struct cairo_ctx {
   int16_t* coef[CAIRO_MAX_COEF_CHUNKS] = {};  // output_cache: slot s in chunk s / coef_per, at s % coef_per
   int coef_chunks = 0, coef_per = 0;
   BlockDesc *table = nullptr, *idesc = nullptr;
-  int32_t* isad = nullptr;
   uint64_t* gran = nullptr;
   uint8_t* rgb = nullptr;
   int16_t* ring_buf = nullptr;
@@ -209,6 +208,7 @@ struct cairo_ctx {
   FrameDesc pend[kMaxBatch];
   int npend = 0;
   int last_slot = -1;  // slot of the last launched frame
+  uint32_t last_epoch = 0;  // and its epoch (the tag of its inter records)
   int wg_rows = 0;
   int wg_helpers = 0;  // helpers of the launch's 2 * wg_rows workgroups (0: half)
   int max_rows = 0;  // row coders (= helpers) per launch that stay co-resident with the other in-flight launch
@@ -308,7 +308,6 @@ EngineArgs engine_args(const cairo_ctx* c) {
   e.plane_elems = c->plane_elems;
   e.table_base = c->table;
   e.idesc_base = c->idesc;
-  e.isad_base = c->isad;
   e.gran_base = c->gran;
   e.sync = c->sync;
   e.sticky = c->sticky;
@@ -441,7 +440,7 @@ void free_ctx(cairo_ctx* c) {
   leave_group(c);
   for (int16_t* q : c->coef)
     if (q) (void)hipFree(q);
-  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->table, (void*)c->idesc, (void*)c->isad, (void*)c->progress, (void*)c->feed_dev, (void*)c->feed_hdr, (void*)c->feed_scratch,
+  for (void* p : {(void*)c->fdesc, (void*)c->order, (void*)c->src, (void*)c->table, (void*)c->idesc, (void*)c->progress, (void*)c->feed_dev, (void*)c->feed_hdr, (void*)c->feed_scratch,
                   (void*)c->gran, (void*)c->rgb, (void*)c->ring_buf, (void*)c->sync, (void*)c->sticky,
                   (void*)c->predeblock, (void*)c->stamps, (void*)c->acct})
     (void)hipFree(p);
@@ -468,7 +467,6 @@ int zero_state(cairo_ctx* c) {
   // inter records: a frame whose search was cut short by a timed-out wait
   // still reads in-frame motion vectors
   CK(hipMemsetAsync(c->idesc, 0, c->nref * c->mbs * sizeof(BlockDesc) * S, c->ks));
-  CK(hipMemsetAsync(c->isad, 0, c->nref * c->mbs * sizeof(int32_t) * S, c->ks));
   // granule tags start at 0; the n-th submission after a reset publishes tag n
   CK(hipMemsetAsync(c->gran, 0, c->mbs * kGranuleStride * sizeof(uint64_t) * S, c->ks));
   CK(hipMemsetAsync(c->sync, 0, c->sync_words * sizeof(int32_t) * kSyncAreas, c->ks));
@@ -645,6 +643,7 @@ int flush(cairo_ctx* c) {
     tb->pending = true;
   }
   const int last = c->pend[e.nframes - 1].slot;
+  const uint32_t last_epoch = c->pend[e.nframes - 1].epoch;
   if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
   hipStream_t pst = c->ps_own ? c->ps : st;
   if (c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
@@ -711,6 +710,7 @@ int flush(cairo_ctx* c) {
     s.launched = true;
   }
   c->last_slot = last;
+  c->last_epoch = last_epoch;
   c->npend = 0;
   c->launched_cv.notify_all();
   return kSuccess;
@@ -865,7 +865,6 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   c->ring_slots = (int)ring;
   TRY(hipMalloc(&c->table, c->mbs * sizeof(BlockDesc) * S));
   TRY(hipMalloc(&c->idesc, c->nref * c->mbs * sizeof(BlockDesc) * S));
-  TRY(hipMalloc(&c->isad, c->nref * c->mbs * sizeof(int32_t) * S));
   TRY(hipMalloc(&c->gran, c->mbs * kGranuleStride * sizeof(uint64_t) * S));
   TRY(hipMalloc(&c->rgb, (size_t)width * height * 3 * S));
   TRY(hipMalloc(&c->sync, c->sync_words * sizeof(int32_t) * kSyncAreas));
@@ -1559,20 +1558,20 @@ int cairo_ctx_read_inter(cairo_ctx* c, uint8_t* descs, int32_t* sads) {
   const size_t n = c->mbs * (c->ring > 1 ? c->ring - 1 : 0);
   if (!n) return kSuccess;
   const size_t o = (size_t)c->last_slot * c->nref * c->mbs;
-  if (CAIRO_TAGGED_RECORDS) {  // two tagged granules per record (kernels.h pack_inter_desc)
-    std::vector<uint64_t> g(2 * n);
-    CK(hipMemcpy(g.data(), c->idesc + o, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < n; i++) {
-      if (descs) {
-        const BlockDesc d = unpack_inter_desc((uint32_t)g[2 * i]);
-        memcpy(descs + i * sizeof(BlockDesc), &d, sizeof(d));
-      }
-      if (sads) sads[i] = (int32_t)(uint32_t)g[2 * i + 1];
+  // two tagged granules per record (kernels.h pack_inter_desc); a record
+  // whose tag is not the last frame's epoch is stale (an intra or decoded
+  // frame has none): refused, not returned as current
+  std::vector<uint64_t> g(2 * n);
+  CK(hipMemcpy(g.data(), c->idesc + o, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < 2 * n; i++)
+    if ((uint32_t)(g[i] >> 32) != c->last_epoch) return kInvalidResource;
+  for (size_t i = 0; i < n; i++) {
+    if (descs) {
+      const BlockDesc d = unpack_inter_desc((uint32_t)g[2 * i]);
+      memcpy(descs + i * sizeof(BlockDesc), &d, sizeof(d));
     }
-    return kSuccess;
+    if (sads) sads[i] = (int32_t)(uint32_t)g[2 * i + 1];
   }
-  if (descs) CK(hipMemcpy(descs, c->idesc + o, n * sizeof(BlockDesc), hipMemcpyDeviceToHost));
-  if (sads) CK(hipMemcpy(sads, c->isad + o, n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return kSuccess;
 }
 
@@ -1590,8 +1589,10 @@ int cairo_ctx_set_debug(cairo_ctx* c, int flags) {
     CK(hipHostGetDevicePointer((void**)&c->trace_dev, c->trace_host, 0));
   }
   if (flags & 8) {
-    const int32_t mark = kWaitHostMark;
-    CK(hipMemcpy(c->sticky, &mark, sizeof(mark), hipMemcpyHostToDevice));
+    int32_t mark[TimeoutInfo::kWords] = {};  // a complete, claimed record
+    mark[TimeoutInfo::kKind] = kWaitHostMark;
+    mark[TimeoutInfo::kClaim] = 1;
+    CK(hipMemcpy(c->sticky, mark, sizeof(mark), hipMemcpyHostToDevice));
   }
   c->inject = (flags & 16) ? 1 : 0;
   if ((flags & 32) && !c->acct) {
@@ -1702,6 +1703,7 @@ int cairo_device_count(void) {
 }
 
 const char* cairo_version(void) { return "cairo_amd 0.1 (gfx950)"; }
+int cairo_api_version(void) { return CAIRO_AMD_API_VERSION; }
 
 }  // extern "C"
 

@@ -38,12 +38,8 @@ constexpr int kGranuleStride = 193;   // + info granule
 // desc} and {epoch, SAD}.  The row coder polls them by tag (no drain and no
 // counter on the helper's side).  The packed desc holds what an inter record
 // can carry: type (3 bits), target (2), sp_pred, sp_amount, sp_index (4), and
-// the motion vector (7 bits each: |mv| <= 31, the search's reach).
-// CAIRO_TAGGED_RECORDS 0: plain stores the helper drains before counting
-// them in inter_done (the round-3 form, kept for A/B timing).
-#ifndef CAIRO_TAGGED_RECORDS
-#define CAIRO_TAGGED_RECORDS 1
-#endif
+// the motion vector (7 bits each: |mv| <= 31, the search's reach).  Intra
+// and decoded frames count their helpers' carrier tasks in inter_done instead.
 __host__ __device__ inline uint32_t pack_inter_desc(const BlockDesc& d) {
   return (d.block_type & 7u) | ((uint32_t)(d.prediction_target & 3) << 3) | ((uint32_t)(d.sp_pred & 1) << 5) |
          ((uint32_t)(d.sp_amount & 1) << 6) | ((uint32_t)(d.sp_index & 15) << 7) |
@@ -93,6 +89,10 @@ struct TimeoutInfo {
   static constexpr int kOn = 6;      // what it waited on: kind-specific (see TimeoutKind)
   static constexpr int kSeenLo = 7;  // the last value it observed, low and high words
   static constexpr int kSeenHi = 8;
+  // Device writers claim the record on kClaim (a CAS), write words 1..8, then
+  // publish kKind last with a release store: a reader that sees kKind set
+  // sees the whole record.
+  static constexpr int kClaim = 9;
   static constexpr int kWords = 16;
 };
 enum TimeoutKind : int32_t {
@@ -194,8 +194,10 @@ struct FrameArgs {
   PlaneSet push[kMaxPush];
   int npush;
   BlockDesc* table;    // [wmb*hmb]
-  BlockDesc* inter_desc;  // [(off-1)*mbs + mb]
-  int32_t* inter_sad;     // [(off-1)*mbs + mb]
+  BlockDesc* inter_desc;  // [(off-1)*mbs + mb]: two tagged granules (desc, SAD) per record
+  // (unused: holds the field offsets -- and so the kernels' scalar-load
+  // merging of this struct -- as measured; dropping it cost 1.3 % at 4K)
+  void* reserved0;
   uint64_t* granules;  // [mbs * kGranuleStride]
   int32_t* err;        // batch error word (a bounded wait timed out)
   int32_t* sticky;     // TimeoutInfo words, never cleared by a launch (reported by the host)
@@ -255,7 +257,6 @@ struct EngineArgs {
   size_t plane_elems;
   BlockDesc* table_base;   // stride mbs
   BlockDesc* idesc_base;   // stride nref * mbs
-  int32_t* isad_base;      // stride nref * mbs
   uint64_t* gran_base;     // stride mbs * kGranuleStride
   int32_t* sync;           // SyncLayout words of this launch
   int32_t* sticky;         // TimeoutInfo words
@@ -290,10 +291,7 @@ struct EngineArgs {
 // at most on frame f-1, row r+3, so any slope > 3 keeps every wait pointing
 // to an earlier key (deadlock-free), while frames interleave in the pools
 // instead of queueing behind each other.
-#ifndef CAIRO_ORDER_SLOPE
-#define CAIRO_ORDER_SLOPE 5
-#endif
-constexpr int kOrderSlope = CAIRO_ORDER_SLOPE;
+constexpr int kOrderSlope = 5;  // (4 and 6 measured slower)
 
 // XCD-banded queues: on a frame of at least kBandMinRows macroblock rows each
 // pool keeps one queue per label (kLabels), and a worker serves the queue of
@@ -309,23 +307,13 @@ constexpr int kOrderSlope = CAIRO_ORDER_SLOPE;
 // 4K A/B: 5387-5391 -> 5483-5486 Mpix/s, engine reads -29 %;
 // at 1080p (68 rows) -1.2 %, so not below kBandMinRows.
 constexpr int kLabels = 8;
-#ifndef CAIRO_BAND_MIN_ROWS
-#define CAIRO_BAND_MIN_ROWS 100
-#endif
-constexpr int kBandMinRows = CAIRO_BAND_MIN_ROWS;
-#ifndef CAIRO_BAND_POOLS
-#define CAIRO_BAND_POOLS 3  // bit 0: the helpers' queues are per label, bit 1: the coders'
-#endif
-constexpr int kBandPools = CAIRO_BAND_POOLS;
-#ifndef CAIRO_BAND_SHIFT
-#define CAIRO_BAND_SHIFT -1  // < 0: contiguous bands of hmb / kLabels rows
-#endif
-#ifndef CAIRO_BAND_ROT
-#define CAIRO_BAND_ROT 5
-#endif
+constexpr int kBandMinRows = 100;
+constexpr int kBandPools = 3;  // bit 0: the helpers' queues are per label, bit 1: the coders'
+// Contiguous bands of hmb / kLabels rows (rotating 4- or 8-row bands read
+// fewer bytes but ran 0.4-0.8 % slower).
 __host__ __device__ inline int task_label(int frame, int row, int hmb) {
-  if (CAIRO_BAND_SHIFT < 0) return row * kLabels / hmb;
-  return ((row >> (CAIRO_BAND_SHIFT < 0 ? 0 : CAIRO_BAND_SHIFT)) + frame * CAIRO_BAND_ROT) & (kLabels - 1);
+  (void)frame;
+  return row * kLabels / hmb;
 }
 
 // A launch's preparation, done by the convert kernel that precedes its

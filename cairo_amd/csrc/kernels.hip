@@ -205,18 +205,8 @@ __device__ __forceinline__ void acquire_fence(bool sys) {
 }
 
 // Poll back-off (s_sleep units of 64 clocks) of the progress-word waits and of
-// the granule re-polls; overridable at build time for sweeps.
-#ifndef CAIRO_WAIT_SLEEP
-#define CAIRO_WAIT_SLEEP 2
-#endif
-#ifndef CAIRO_GRAN_SLEEP
-#define CAIRO_GRAN_SLEEP 1
-#endif
-// Deblock readiness (and the helper's progress poll): the words tested loaded together (1) or one after
-// the other (0).
-#ifndef CAIRO_READY_PAIR
-#define CAIRO_READY_PAIR 1
-#endif
+// the granule re-polls (sweeps of 0-3 were within noise).
+constexpr int kWaitSleep = 2, kGranSleep = 1;
 
 // A bounded wait gave up (~2 s): set the launch's error word, so that every
 // other wait ends and every workgroup drains (the host then reports
@@ -228,11 +218,14 @@ __device__ __attribute__((noinline)) void report_timeout(int32_t* err, int32_t* 
                                                          uint64_t seen) {
   __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int32_t none = 0;
-  if (!__hip_atomic_compare_exchange_strong(sticky + TimeoutInfo::kKind, &none, kind, __ATOMIC_RELAXED,
+  if (!__hip_atomic_compare_exchange_strong(sticky + TimeoutInfo::kClaim, &none, 1, __ATOMIC_RELAXED,
                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
     return;  // an earlier timeout is the one reported
   const int32_t w[8] = {(int32_t)epoch, index, row, member, need, on, (int32_t)(uint32_t)seen, (int32_t)(seen >> 32)};
   for (int k = 0; k < 8; k++) __hip_atomic_store(sticky + 1 + k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the kind last: readers (k_feed_copy, the host's D2H, cairo_ctx_timeout_info)
+  // take a set kind as the record's completion
+  __hip_atomic_store(sticky + TimeoutInfo::kKind, kind, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void report_timeout(FA& a, int kind, int row, int need, int on, uint64_t seen) {
   report_timeout(a.err, a.sticky, kind, a.epoch, a.index, row, a.member, need, on, seen);
@@ -247,7 +240,7 @@ __device__ __forceinline__ void wait_records(FA& a, int row, int group) {
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while ((v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < a.nref) {
     if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
+    __builtin_amdgcn_s_sleep(kWaitSleep);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
       report_timeout(a, kWaitRecords, row, a.nref, group, (uint32_t)v);
       return;
@@ -284,7 +277,7 @@ __device__ __forceinline__ uint32_t rec_settle(FA& a, const uint64_t* p, uint64_
   if ((uint32_t)(g >> 32) == a.epoch) return (uint32_t)g;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
+    __builtin_amdgcn_s_sleep(kWaitSleep);
     g = gran_ld(p);
     if (CAIRO_ACCT && a.acct) {
       const uint64_t act = __ballot(1);
@@ -309,7 +302,7 @@ __device__ __forceinline__ uint32_t gran_settle(FA& a, const uint64_t* p, uint64
   if ((uint32_t)(g >> 32) == a.epoch) return (uint32_t)g;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    __builtin_amdgcn_s_sleep(CAIRO_GRAN_SLEEP);
+    __builtin_amdgcn_s_sleep(kGranSleep);
     g = gran_ld(p);
     if (CAIRO_ACCT && a.acct) {  // this wave's re-poll: 8 bytes per active lane
       const uint64_t act = __ballot(1);
@@ -423,15 +416,9 @@ __device__ __forceinline__ void pk_diff(uint32_t a, uint32_t b, uint32_t& sad, u
 // every candidate the searches can reach.
 // ---------------------------------------------------------------------------
 
-// Luma pitch: 136 elements = 68 dwords puts rows i and i+8 of a candidate's
-// 16-lane group on one bank (ds_read_b32 banks are dword mod 32); 140 = 70
-// dwords spreads 16 rows over 16 banks, at the price of 8-byte (not 16-byte)
-// aligned rows for the staging stores.
-#ifndef CAIRO_WIN_PITCH
-#define CAIRO_WIN_PITCH 136
-#endif
-constexpr int kWinL = 80, kWinLW = 128, kWinLP = CAIRO_WIN_PITCH;  // luma rows, width, pitch (elements)
-static_assert(kWinLP % 4 == 0 || kWinLP % 4 == 2, "window rows 4- or 8-byte aligned");
+// Luma pitch: 136 elements (68 dwords): window rows stay 16-byte aligned for
+// the 16-byte LDS-DMA (dma_window) and hold a 128-column row plus a pad.
+constexpr int kWinL = 80, kWinLW = 128, kWinLP = 136;  // luma rows, width, pitch (elements)
 constexpr int kWinC = 40, kWinCP = 72;  // chroma rows, pitch (64 columns)
 
 struct alignas(16) Window {
@@ -447,143 +434,54 @@ __device__ __forceinline__ uint4 bias4(uint4 v) {
   return v;
 }
 
-// Stage the in-frame part of window rows [r0, r1) x columns [c0, c1) (luma;
-// columns multiples of 16; chroma rows [r0/2, r1/2), columns halved) with
-// origin (ox, oy) (luma pixels, multiples of 16) from plane set p, biased.
-// All 256 threads participate.
-#ifndef CAIRO_WIN_UNROLL
-#define CAIRO_WIN_UNROLL 2
-#endif
-constexpr int kWinUnroll = CAIRO_WIN_UNROLL;
-
 // Traffic attribution builds (tools/attr_traffic.sh; never a product build):
 // bit 0 skips the search-window loads (the windows hold stale LDS), bit 2 the
 // row coder's inter-prediction loads (constant predictions).  The searches and
 // codes then run on wrong data -- same task shapes, wrong results -- so the
 // drop in fabric reads against the default build is what those loads cost.
+// Refused unless the build says it is a tools build.
 #ifndef CAIRO_ATTR_SKIP
 #define CAIRO_ATTR_SKIP 0
 #endif
-__device__ __forceinline__ void load_window(Window& w, const PlaneSet& p, int wa, int ha, int ox,
-                                            int oy, int r0, int r1, int c0, int c1) {
-  if (CAIRO_ATTR_SKIP & 1) return;
-  // All of a thread's 16-byte loads are issued before the first LDS store
-  // (kWinUnroll in flight): the staging costs one fabric round trip instead
-  // of one per chunk.  Chunks are numbered over whole window rows (16 per
-  // luma row, 8 per chroma row) and those outside [c0, c1) skipped, so that
-  // a chunk's row and column are shifts, not divisions.
-  const int nl = (r1 - r0) << 4;
-  const int cr0 = r0 >> 1, ncl = ((r1 >> 1) - cr0) << 3;  // chroma rows [r0/2, r1/2)
-  const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
-  const int n = nl + 2 * ncl;
-  for (int k0 = threadIdx.x; k0 < n; k0 += 256 * kWinUnroll) {
-    uint4 v[kWinUnroll];
-    int16_t* dst[kWinUnroll];
-#pragma unroll
-    for (int u = 0; u < kWinUnroll; u++) {
-      const int k = k0 + 256 * u;
-      dst[u] = nullptr;
-      if (k < nl) {
-        const int r = r0 + (k >> 4), c = (k & 15) << 3;
-        const int gy = oy + r, gx = ox + c;
-        if (c >= c0 && c < c1 && gy >= 0 && gy < ha && gx >= 0 && gx < wa) {
-          v[u] = *(const uint4*)&p.y[(size_t)gy * wa + gx];
-          dst[u] = &w.y[r * kWinLP + c];
-        }
-      } else if (k < n) {
-        const int kc = k - nl, pl = kc >= ncl, kk = kc - (pl ? ncl : 0);
-        const int r = cr0 + (kk >> 3), c = (kk & 7) << 3;
-        const int gy = coy + r, gx = cox + c;
-        if (2 * c >= c0 && 2 * c < c1 && gy >= 0 && gy < ch && gx >= 0 && gx < cw) {
-          v[u] = *(const uint4*)&pick(p, 1 + pl)[(size_t)gy * cw + gx];
-          dst[u] = &(pl ? w.v : w.u)[r * kWinCP + c];
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kWinUnroll; u++)
-      if (dst[u]) {
-        const uint4 b = bias4(v[u]);
-        if (kWinLP % 8 == 0) {
-          *(uint4*)dst[u] = b;
-        } else {  // 8-byte aligned rows (chroma rows stay 16-byte aligned; the same stores serve both)
-          ((uint2*)dst[u])[0] = make_uint2(b.x, b.y);
-          ((uint2*)dst[u])[1] = make_uint2(b.z, b.w);
-        }
-      }
-  }
-}
-
-// The same staging by LDS-DMA (global_load_lds: no VGPR destination, so every
-// load of the window is in flight at once -- one fabric round trip instead of
-// one per kWinUnroll loads), then an in-LDS pass that biases the staged
-// region.  One wave instruction stages one window row: luma 64 lanes x 4 B
-// (128 columns, pitch kWinLP), chroma 32 lanes x 4 B (64 columns, pitch
-// kWinCP): an LDS-DMA writes wave-uniform base + lane x 4, so each row's
-// padding stays outside.  Rows outside the frame are skipped; lanes whose
-// columns fall outside [c0, c1) or the frame are masked off.  All 256 threads
-// participate; ends with the bias pass's writes issued (the caller's barrier
-// publishes them).
-#ifndef CAIRO_WIN_DMA
-#define CAIRO_WIN_DMA 2
+#if CAIRO_ATTR_SKIP && !defined(CAIRO_TOOLS_BUILD)
+#error "CAIRO_ATTR_SKIP produces wrong output: tools builds only (define CAIRO_TOOLS_BUILD)"
 #endif
+
+// Stage the in-frame part of window rows [r0, r1) x columns [c0, c1) (luma;
+// columns multiples of 16; chroma rows [r0/2, r1/2), columns halved) with
+// origin (ox, oy) (luma pixels, multiples of 16) from plane set p by LDS-DMA
+// (global_load_lds: no VGPR destination, so every load of the window is in
+// flight at once -- one fabric round trip), 16 bytes per lane: the window's
+// rows are numbered as 16-byte chunks over the PADDED pitch (17 per luma row,
+// 9 per chroma row), so one wave instruction fills 64 consecutive chunks
+// (~3.8 luma rows) and the lanes that land in a row's pad, outside [c0, c1)
+// or outside the frame are masked off (an LDS-DMA writes wave-uniform base +
+// lane x 16).  All 256 threads participate; the values land raw (bias_window
+// follows).
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void dma_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
                                            int r1, int c0, int c1) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (CAIRO_ATTR_SKIP & 1) return;
-  if (CAIRO_WIN_DMA == 2) {
-    // 16-byte lanes: the window's rows are numbered as 16-byte chunks over the
-    // PADDED pitch (17 per luma row, 9 per chroma row), so one wave
-    // instruction fills 64 consecutive chunks (~3.8 luma rows) and the lanes
-    // that land in a row's pad, outside [c0, c1) or outside the frame are
-    // masked off: as many wave instructions as the register staging, every one
-    // in flight at once.
-    constexpr int kLC = kWinLP / 8, kCC = kWinCP / 8;
-    static_assert(kWinLP % 8 == 0 && kWinCP % 8 == 0, "16-byte chunked pitches");
-    const int k0 = r0 * kLC, k1 = r1 * kLC;
-    for (int kb = k0 + 64 * wave; kb < k1; kb += 256) {
-      const int k = kb + lane, r = k / kLC, cc = k - r * kLC, c = cc << 3;
-      const int gy = oy + r, gx = ox + c;
-      if (k < k1 && cc < (kWinLW >> 3) && c >= c0 && c < c1 && gy >= 0 && gy < ha && gx >= 0 && gx < wa)
-        __builtin_amdgcn_global_load_lds((const void*)&p.y[(size_t)gy * wa + gx], (lds_void*)&w.y[kb << 3], 16, 0, 0);
-    }
-    const int cr0 = r0 >> 1, cr1 = r1 >> 1, ck0 = cr0 * kCC, ck1 = cr1 * kCC;
-    const int ni = (ck1 - ck0 + 63) >> 6;  // instructions per chroma plane
-    const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
-    for (int i = wave; i < 2 * ni; i += 4) {
-      const int pl = i >= ni, kb = ck0 + ((i - (pl ? ni : 0)) << 6);
-      const int k = kb + lane, r = k / kCC, cc = k - r * kCC, c = cc << 3;
-      const int gy = coy + r, gx = cox + c;
-      if (k < ck1 && cc < 8 && 2 * c >= c0 && 2 * c < c1 && gy >= 0 && gy < ch && gx >= 0 && gx < cw)
-        __builtin_amdgcn_global_load_lds((const void*)&pick(p, 1 + pl)[(size_t)gy * cw + gx],
-                                         (lds_void*)&(pl ? w.v : w.u)[kb << 3], 16, 0, 0);
-    }
-    return;
+  constexpr int kLC = kWinLP / 8, kCC = kWinCP / 8;
+  static_assert(kWinLP % 8 == 0 && kWinCP % 8 == 0, "16-byte chunked pitches");
+  const int k0 = r0 * kLC, k1 = r1 * kLC;
+  for (int kb = k0 + 64 * wave; kb < k1; kb += 256) {
+    const int k = kb + lane, r = k / kLC, cc = k - r * kLC, c = cc << 3;
+    const int gy = oy + r, gx = ox + c;
+    if (k < k1 && cc < (kWinLW >> 3) && c >= c0 && c < c1 && gy >= 0 && gy < ha && gx >= 0 && gx < wa)
+      __builtin_amdgcn_global_load_lds((const void*)&p.y[(size_t)gy * wa + gx], (lds_void*)&w.y[kb << 3], 16, 0, 0);
   }
-  {  // luma: rows r0 + wave, r0 + wave + 4, ...; lane = column pair
-    const int c = 2 * lane, gx = ox + c;
-    const bool col_ok = c >= c0 && c < c1 && gx >= 0 && gx < wa;
-    for (int r = r0 + wave; r < r1; r += 4) {
-      const int gy = oy + r;
-      if (gy < 0 || gy >= ha) continue;  // wave-uniform
-      if (col_ok)
-        __builtin_amdgcn_global_load_lds((const void*)&p.y[(size_t)gy * wa + gx], (lds_void*)&w.y[r * kWinLP], 4, 0, 0);
-    }
-  }
-  {  // chroma: U rows then V rows, [r0/2, r1/2); lanes 0..31 = column pairs
-    // (an LDS-DMA writes lane x 4 bytes whatever the load size, so a 64-column
-    // chroma row is 32 dword lanes; the upper half-wave idles)
-    const int cr0 = r0 >> 1, cr1 = r1 >> 1, ncr = cr1 - cr0;
-    const int cw = wa >> 1, ch = ha >> 1, cx = 2 * lane, gx = (ox >> 1) + cx;
-    const bool col_ok = lane < 32 && 2 * cx >= c0 && 2 * cx < c1 && gx >= 0 && gx < cw;
-    for (int k = wave; k < 2 * ncr; k += 4) {
-      const int pl = k >= ncr, r = cr0 + k - (pl ? ncr : 0), gy = (oy >> 1) + r;
-      if (gy < 0 || gy >= ch) continue;
-      if (col_ok)
-        __builtin_amdgcn_global_load_lds((const void*)&pick(p, 1 + pl)[(size_t)gy * cw + gx],
-                                         (lds_void*)&(pl ? w.v : w.u)[r * kWinCP], 4, 0, 0);
-    }
+  const int cr0 = r0 >> 1, cr1 = r1 >> 1, ck0 = cr0 * kCC, ck1 = cr1 * kCC;
+  const int ni = (ck1 - ck0 + 63) >> 6;  // instructions per chroma plane
+  const int cw = wa >> 1, ch = ha >> 1, cox = ox >> 1, coy = oy >> 1;
+  for (int i = wave; i < 2 * ni; i += 4) {
+    const int pl = i >= ni, kb = ck0 + ((i - (pl ? ni : 0)) << 6);
+    const int k = kb + lane, r = k / kCC, cc = k - r * kCC, c = cc << 3;
+    const int gy = coy + r, gx = cox + c;
+    if (k < ck1 && cc < 8 && 2 * c >= c0 && 2 * c < c1 && gy >= 0 && gy < ch && gx >= 0 && gx < cw)
+      __builtin_amdgcn_global_load_lds((const void*)&pick(p, 1 + pl)[(size_t)gy * cw + gx],
+                                       (lds_void*)&(pl ? w.v : w.u)[kb << 3], 16, 0, 0);
   }
 }
 // Bias window rows [r0, r1) x columns [c0, c1) in LDS (v ^ 0x8000), in
@@ -623,10 +521,7 @@ __device__ __forceinline__ void acct_window(uint64_t* acct, int r0, int r1, int 
 }
 __device__ __forceinline__ void stage_window(Window& w, const PlaneSet& p, int wa, int ha, int ox, int oy, int r0,
                                              int r1, int c0, int c1) {
-  if (CAIRO_WIN_DMA)
-    load_window_dma(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
-  else
-    load_window(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
+  load_window_dma(w, p, wa, ha, ox, oy, r0, r1, c0, c1);
 }
 
 // Per-lane slice of a macroblock: luma row l>>2, columns (l&3)*4..+3, and the
@@ -914,21 +809,6 @@ __device__ __forceinline__ BlockDesc make_desc(const Sel& s, int px, int py, int
 // So a frame follows its predecessor at MB row r+2, 5-6 macroblocks ahead.
 constexpr int kLvl1Rows = 77, kLvl1Cols = 112;
 
-#ifndef CAIRO_HELPER_INTERLEAVE
-#define CAIRO_HELPER_INTERLEAVE 1
-#endif
-constexpr bool kHelperInterleave = CAIRO_HELPER_INTERLEAVE;
-// The in-place deblock of a row is run by its row coder, in the waits for its
-// inter records (and at the end of the row), instead of by its helper: the
-// helpers' searches pace the rows, the coders wait for them.
-#ifndef CAIRO_CODER_DEBLOCK
-#define CAIRO_CODER_DEBLOCK 0
-#endif
-constexpr bool kCoderDeblock = CAIRO_CODER_DEBLOCK;
-// Inter records as tagged granules (kernels.h CAIRO_TAGGED_RECORDS).
-constexpr bool kTaggedRecords = CAIRO_TAGGED_RECORDS && !CAIRO_CODER_DEBLOCK;
-static_assert(!(CAIRO_TAGGED_RECORDS && CAIRO_CODER_DEBLOCK), "the coder-side deblock waits on inter_done");
-
 // Thread 0's value v, broadcast to the workgroup (two barriers).
 __device__ __forceinline__ int wg_broadcast(volatile int* slot, int v) {
   if (threadIdx.x == 0) *slot = v;
@@ -947,45 +827,28 @@ __device__ __forceinline__ bool deblock_pending(FA& a, const DbState& st);
 
 // Helper wait (whole workgroup): until the deblock progress of frame
 // index-back (back = 1: the previous frame, 2: the one before) of MB row rr
-// reaches need, running this row's ready deblock chunks meanwhile; then
-// acquire what the progress word released.  Bounded like every wait (the
-// error word ends it).  full (LDS, optional): also whether rows rr and r+3
-// are final through full_cols (the whole search window, inter_task), from
-// the same polls -- covered by the same acquire.
+// reaches need, running this row's ready deblock chunks meanwhile (kDeblock);
+// then acquire what the progress word released.  Bounded like every wait (the
+// error word ends it).
 template <bool kDeblock = true>
-__device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int need, DbLds& D,
-                                            DbState& st, int* flag, int* full = nullptr, int full_cols = 0) {
+__device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int need, DbLds& D, DbState& st,
+                                            int* flag) {
   volatile int* vflag = flag;
   const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
-  const int r3 = min(r + 3, a.hmb - 1);
   uint64_t t0 = 0;
   const uint64_t ta = acct_now();
   uint64_t tdb = 0;  // accounting: time in deblock chunks run here
   for (;;) {
     int d = 0;
     if (threadIdx.x == 0) {
-#if CAIRO_READY_PAIR
       // the progress poll and the deblock readiness loads in flight together
       const uint64_t pv = pp ? progress_peer(a.sys, pp + rr) : ~0ull;
-      const uint64_t p3 = pp && full ? progress_peer(a.sys, pp + r3) : ~0ull;
-      const bool dbr = kDeblock && !kCoderDeblock && kHelperInterleave && deblock_pending(a, st) &&
-                       deblock_chunk_ready(a, r, st);
-#else
-      const uint64_t p3 = pp && full ? progress_peer(a.sys, pp + r3) : ~0ull;
-      const uint64_t pv = pp ? progress_peer(a.sys, pp + rr) : ~0ull;
-      const bool dbr = pv < tagged(a.epoch - back, need) && kDeblock && !kCoderDeblock && kHelperInterleave &&
-                       deblock_pending(a, st) && deblock_chunk_ready(a, r, st);
-#endif
+      const bool dbr = kDeblock && deblock_pending(a, st) && deblock_chunk_ready(a, r, st);
       if (a.inject && r == min(1, a.hmb - 1)) {  // test hook: this wait "times out" at once
         report_timeout(a, kWaitInjected, r, need, rr | (back << 16), pv);
         d = 1;
-        if (full) *(volatile int*)full = 0;
       } else if (pv >= tagged(a.epoch - back, need)) {
         d = 1;
-        if (full) {
-          const uint64_t want = tagged(a.epoch - back, full_cols);
-          *(volatile int*)full = (pv >= want) & (p3 >= want);
-        }
       } else if (dbr) {
         d = 2;
       } else {  // nothing to do: back off
@@ -998,7 +861,6 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
           report_timeout(a, kWaitPrevProgress, r, need, rr | (back << 16), pv);
           d = 1;
         }
-        if (d && full) *(volatile int*)full = 0;
       }
     }
     d = wg_broadcast(vflag, d);
@@ -1017,32 +879,6 @@ __device__ __forceinline__ void helper_wait(FA& a, int back, int r, int rr, int 
   acct_add(a.acct, Acct::kHelperWait, acct_now() - ta - tdb);
 }
 
-#ifndef CAIRO_DB_IN_WAIT1
-#define CAIRO_DB_IN_WAIT1 1
-#endif
-
-#ifndef CAIRO_GROUP_SOURCE
-#define CAIRO_GROUP_SOURCE 1
-#endif
-constexpr bool kGroupSource = CAIRO_GROUP_SOURCE;
-// The row helper's group source double-buffered in LDS: group g+1's four
-// macroblocks staged by LDS-DMA (one instruction per wave) at group g's start,
-// in flight with g's progress poll whose wait covers them, instead of a
-// register load round trip at each group's start.  Bit-exact, measured
-// neutral at 4K (5784 vs 5782, profiles/r04/ab_4k_n.txt): off, and then the
-// second buffer is not allocated.
-#ifndef CAIRO_HSRC_DMA
-#define CAIRO_HSRC_DMA 0
-#endif
-constexpr bool kHelperSrcDma = CAIRO_HSRC_DMA && CAIRO_GROUP_SOURCE;
-// Window DMA issued before the zero-MV loads (one round trip for both), with
-// the whole-window finality taken from the preceding helper_wait (1), or
-// staged after the zero-MV check (0).
-#ifndef CAIRO_SPEC_STAGE
-#define CAIRO_SPEC_STAGE 0
-#endif
-constexpr bool kSpecStage = CAIRO_SPEC_STAGE && CAIRO_WIN_DMA != 0 && CAIRO_GROUP_SOURCE;
-
 struct InterLds {
   Window win;
   int need[4];
@@ -1051,7 +887,7 @@ struct InterLds {
   // the group's source macroblocks (raw int16: 16x16 luma, 8x8 U, 8x8 V per
   // wave), loaded once per group; the zero-MV SAD / MAD of the older
   // references, computed together at the group start
-  alignas(16) int16_t src[kHelperSrcDma ? 2 : 1][4][384];  // kHelperSrcDma: by group g & 1 (g+1 staged during g)
+  alignas(16) int16_t src[4][384];
   int zsad[kMaxRing][4], zmad[kMaxRing][4];
 };
 
@@ -1059,7 +895,7 @@ struct InterLds {
 // 16 x 16, then U 8 x 8, then V 8 x 8; lanes 0..47 one 16-byte chunk each (a
 // luma half row, a chroma row).  Only this wave reads it back (its LDS
 // operations execute in order: no barrier).
-__device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L, bool dma = false) {
+__device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, x = 4 * g + wave;
   if (x >= a.wmb || lane >= 48) return;
   const PlaneSet in = planes(a.in);
@@ -1071,10 +907,7 @@ __device__ __forceinline__ void group_source(FA& a, int r, int g, InterLds& L, b
     const int k = lane - 32;
     gsrc = pick(in, 1 + (k >> 3)) + (size_t)((py >> 1) + (k & 7)) * (a.wa >> 1) + (px >> 1);
   }
-  if (dma)  // one LDS-DMA instruction per wave: lane l lands at + 16 l, the layout above
-    __builtin_amdgcn_global_load_lds((const void*)gsrc, (lds_void*)&L.src[g & kHelperSrcDma][wave][0], 16, 0, 0);
-  else
-    *(uint4*)&L.src[g & kHelperSrcDma][wave][8 * lane] = *(const uint4*)gsrc;
+  *(uint4*)&L.src[wave][8 * lane] = *(const uint4*)gsrc;
 }
 
 // Macroblock (x, r)'s source into dst (group_source's layout) by ONE LDS-DMA
@@ -1095,9 +928,9 @@ __device__ __forceinline__ void src_dma(FA& a, int x, int r, int16_t* dst) {
 
 // This lane's Px6 slice (px_from_planes layout) and its SrcRow (load_src_rows
 // layout, biased) of wave w's source macroblock, from L.src.
-__device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
+__device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int wave) {
   const int l = threadIdx.x & 63;
-  const int16_t* m = L.src[g & kHelperSrcDma][wave];
+  const int16_t* m = L.src[wave];
   Px6 p;
   const int16_t* y = &m[(l >> 2) * 16 + (l & 3) * 4];
   p.y0 = y[0], p.y1 = y[1], p.y2 = y[2], p.y3 = y[3];
@@ -1105,8 +938,8 @@ __device__ __forceinline__ Px6 src_px_lds(const InterLds& L, int g, int wave) {
   p.v = m[320 + (l >> 3) * 8 + (l & 7)];
   return p;
 }
-__device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int g, int wave, int i) {
-  const uint32_t* m = (const uint32_t*)L.src[g & kHelperSrcDma][wave];
+__device__ __forceinline__ SrcRow src_rows_lds(const InterLds& L, int wave, int i) {
+  const uint32_t* m = (const uint32_t*)L.src[wave];
   SrcRow s;
 #pragma unroll
   for (int k = 0; k < 8; k++) s.y[k] = m[i * 8 + k] ^ 0x80008000u;
@@ -1124,7 +957,7 @@ __device__ __forceinline__ void zero_mv_older(FA& a, int r, int g, InterLds& L) 
   acct_add(a.acct, Acct::kZeroMvBytes, 768ull * (a.nref - 1) * (uint64_t)min(4, a.wmb - 4 * g));
   if (x >= a.wmb) return;
   const int px = x * kMB, py = r * kMB;
-  const Px6 src = src_px_lds(L, g, wave);
+  const Px6 src = src_px_lds(L, wave);
   Px6 ref[kMaxRing - 1];
 #pragma unroll
   for (int off = 2; off < kMaxRing; off++)
@@ -1144,17 +977,10 @@ __device__ __forceinline__ int inter_need_cols(FA& a, int g, int level) {
   return min(64 * g + (level == 1 ? 80 : 96), a.wa);
 }
 
-// publish = 0: the task's records stay in flight (a later task of the group
-// drains them); publish = n: drain this wave's stores and add n to the group's
-// finished count (the coder waits for nref).
-// hint >= 0: whether the reference is final over the whole window, as the
-// caller's helper_wait found (with its acquire); the task then skips its own
-// check.  staged: the caller has issued the window's DMA for this reference
-// (whole window if hint, else level 1) before the zero-MV loads, which waited
-// for it; only the bias pass remains (kSpecStage).
-__device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLds& L, DbLds& D,
-                                           DbState& st, int* flag, uint64_t* is, int publish, int hint = -1,
-                                           bool staged = false) {
+// Reference offset `off` of group g of row r: the tagged records of the
+// group's macroblocks are stored and left in flight (the coder polls them).
+__device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLds& L, DbLds& D, DbState& st,
+                                           int* flag, uint64_t* is) {
   const int wave = uni(threadIdx.x >> 6);  // scalar: the acceptance replay runs on SGPRs
   const int x = 4 * g + wave;
   const bool valid = x < a.wmb;
@@ -1171,29 +997,18 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   s.sad = s.mad = 0;
   SrcRow srow;  // biased source rows of this lane's group slot (integer steps)
   const int ox = 4 * g * kMB - 32, oy = py - 32;  // window origin
-  if (kSpecStage && hint >= 0 && off == 1) {
-    // the window in flight with the zero-MV loads below (one round trip for
-    // both); discarded if no macroblock needs the search
-    dma_window(L.win, ref, a.wa, a.ha, ox, oy, 0, hint ? kWinL : kLvl1Rows, 0, hint ? kWinLW : kLvl1Cols);
-    staged = true;
-  }
-  if (valid && kGroupSource) {  // the source from the group's LDS copy
-    src = src_px_lds(L, g, wave);
-    srow = src_rows_lds(L, g, wave, threadIdx.x & 15);
+  if (valid) {  // the source from the group's LDS copy
+    src = src_px_lds(L, wave);
+    srow = src_rows_lds(L, wave, threadIdx.x & 15);
     if (off >= 2) {  // zero-MV computed at the group start
       s.sad = L.zsad[off][wave], s.mad = L.zmad[off][wave];
     } else {  // zero-MV candidate straight from the planes
       sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
     }
-  } else if (valid) {  // zero-MV candidate straight from the planes
-    src = px_from_planes(planes(a.in), a.wa, px, py);
-    sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
-    srow = load_src_rows(planes(a.in), a.wa, px, py, threadIdx.x & 15);
   }
   const bool need = valid && s.mad >= thr;
   if ((threadIdx.x & 63) == 0) L.need[wave] = need;
-  if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's window DMA has landed
-  if (hint < 0 && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     // Is the reference already final over the whole window (level 2 too)?
     // Always, in practice, for the older references (frame index-2 runs far
     // ahead): then the window is staged in one go and the steps skip the
@@ -1201,15 +1016,10 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
     const int back = off == 1 ? 1 : 2;
     const uint64_t* pp = back == 1 ? a.prev_progress : a.prev2_progress;
     const uint64_t want = tagged(a.epoch - back, inter_need_cols(a, g, 2));
-#if CAIRO_READY_PAIR
     // both words loaded before either is tested (one round trip)
     const uint64_t w3 = pp ? progress_peer(a.sys, pp + min(r + 3, a.hmb - 1)) : 0;
     const uint64_t w2 = pp ? progress_peer(a.sys, pp + min(r + 2, a.hmb - 1)) : 0;
     const int full = !pp || ((w3 >= want) & (w2 >= want));
-#else
-    const int full = !pp || (progress_peer(a.sys, pp + min(r + 3, a.hmb - 1)) >= want &&
-                             progress_peer(a.sys, pp + min(r + 2, a.hmb - 1)) >= want);
-#endif
     if (full && pp) {  // acquire what the progress words released (the loads below follow the barrier)
       acquire_fence(a.sys);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1220,16 +1030,11 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   if (is && off == 1) is[3] = __builtin_amdgcn_s_memrealtime();
   acct_add(a.acct, Acct::kInterTasks, 1);
   acct_add(a.acct, Acct::kZeroMvBytes, (off == 1 ? 768ull : 0ull) * (uint64_t)min(4, a.wmb - 4 * g));
-  if (CAIRO_ACCT && !(L.need[0] | L.need[1] | L.need[2] | L.need[3]) && staged)
-    acct_add(a.acct, Acct::kWinSpecUnused, (uint64_t)(L.full ? kWinL * kWinLW : kLvl1Rows * kLvl1Cols) * 3);
   if (L.need[0] | L.need[1] | L.need[2] | L.need[3]) {
     const bool full = L.full != 0;  // workgroup-uniform
     acct_add(a.acct, Acct::kSearchedTasks, 1);
     acct_window(a.acct, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
-    if (staged)
-      bias_window(L.win, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
-    else
-      stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
+    stage_window(L.win, ref, a.wa, a.ha, ox, oy, 0, full ? kWinL : kLvl1Rows, 0, full ? kWinLW : kLvl1Cols);
     __syncthreads();
     if (is && off == 1) is[4] = __builtin_amdgcn_s_memrealtime();
     bool lvl2c = full, lvl2r = full;  // workgroup-uniform
@@ -1363,41 +1168,18 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
   }
   if (is && off == 1) is[10] = __builtin_amdgcn_s_memrealtime();
   if (valid && (threadIdx.x & 63) == 0) {
+    // two tagged granules (kernels.h pack_inter_desc): the coder polls them,
+    // so nothing waits for these stores
     const BlockDesc d = make_desc(s, px, py, thr, false, off);
-    if (kTaggedRecords) {
-      // two tagged granules (kernels.h pack_inter_desc): the coder polls them,
-      // so nothing waits for these stores
-      uint64_t* rec = (uint64_t*)&a.inter_desc[(off - 1) * mbs + mb];
-      const uint64_t tag = (uint64_t)a.epoch << 32;
-      gran_st(rec, tag | pack_inter_desc(d));
-      gran_st(rec + 1, tag | (uint32_t)s.sad);
-    } else {
-      // Write-through (sc1) stores: complete at the coherence point once vmcnt
-      // drains, so the counter below is published without a release fence,
-      // whose L2 write-back (buffer_wbl2) per reference and group cost 9 % at
-      // 4K (MI355X_MICROARCH.md R2; the coder acquires after its wait).
-      uint32_t wd[4];
-      memcpy(wd, &d, sizeof(wd));
-      gbl_u32* dst = (gbl_u32*)&a.inter_desc[(off - 1) * mbs + mb];
-#pragma unroll
-      for (int k = 0; k < 4; k++) __hip_atomic_store(dst + k, wd[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gbl_u32*)&a.inter_sad[(off - 1) * mbs + mb], (uint32_t)s.sad, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
+    uint64_t* rec = (uint64_t*)&a.inter_desc[(off - 1) * mbs + mb];
+    const uint64_t tag = (uint64_t)a.epoch << 32;
+    gran_st(rec, tag | pack_inter_desc(d));
+    gran_st(rec + 1, tag | (uint32_t)s.sad);
   }
-  if (publish && !kTaggedRecords) {
-    // all records of the group's tasks stored (vmcnt counts every store of
-    // the wave, earlier tasks' included); release them to the row coder
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(&a.inter_done[r * a.ng + g], publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    // the next task rewrites the window: every wave is done reading it (its
-    // LDS reads returned); the records' stores stay in flight (each one waits
-    // about 3.5 us for its write-through acknowledgement)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
+  // the next task rewrites the window: every wave is done reading it (its
+  // LDS reads returned); the records' stores stay in flight (each one waits
+  // about 3.5 us for its write-through acknowledgement)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -1587,28 +1369,11 @@ __device__ __forceinline__ int edge_strength_q(int l, int r, int& qp) {
 // chunk ahead; a chunk runs only once its inputs are present (the helper
 // interleaves it with the inter search), so a wide chunk delays the row's
 // progress but never stalls the helper.
-// The chunk width is per frame (FrameArgs::db_shift, make_frame_view): 0
-// picks it by frame width, CAIRO_DB_CHUNK = 16 / 32 / 64 forces one.
-#ifndef CAIRO_DB_CHUNK
-#define CAIRO_DB_CHUNK 0
-#endif
+// The chunk width is per frame (FrameArgs::db_shift, make_frame_view), by
+// frame width.
 constexpr int kDbChunk = 64;  // the widest chunk: luma columns (tile width, info table, arrays)
 constexpr int kDbMBs = kDbChunk / 16;
 __device__ __forceinline__ int db_chunks(const FA& a) { return (a.wa + (1 << a.db_shift) - 1) >> a.db_shift; }
-// The deblock's 4 rows above loaded all at once (1: one round trip) or one
-// load per pass of the lanes (0: the round-3 form, a round trip per pass).
-#ifndef CAIRO_ABOVE_BATCH
-#define CAIRO_ABOVE_BATCH 1
-#endif
-// The filters of a 64-column chunk over all four waves (1: a workgroup
-// barrier between the four phases) or in wave 0 (0: its LDS operations run in
-// order, no barriers; the other waves go on to the write-out's barrier).
-// Round 4, 4K: 0 is +0.3 % over five alternating rounds
-// (profiles/r04/ab_4k_s.txt, ab_4k_t.txt).
-#ifndef CAIRO_DB_SPREAD
-#define CAIRO_DB_SPREAD 0
-#endif
-constexpr bool kDbSpread = CAIRO_DB_SPREAD;
 constexpr int kDbLW = 128, kDbLP = 130;  // luma tile columns (circular), pitch
 constexpr int kDbCW = 64, kDbCP = 66;    // chroma
 
@@ -1645,20 +1410,11 @@ __device__ __forceinline__ const uint64_t* gran_mb(FA& a, int mbx, int mby) {
   return a.granules + (size_t)(mby * a.wmb + mbx) * kGranuleStride;
 }
 
-// Per-phase deblock times in the stamps (tools/k2_phases.py); off by default:
-// the extra live values cost VGPR spills.
-#ifndef CAIRO_DB_PHASES
-#define CAIRO_DB_PHASES 0
-#endif
-
 // Deblock progress of one MB row: next chunk, columns written, band B's next
 // H column and next V unit.
 struct DbState {
   int k, w0, hb0, vb0;
   uint64_t busy = 0;  // diagnostic: time in deblock_chunk (thread 0, 10 ns ticks; only with stamps)
-#if CAIRO_DB_PHASES
-  uint64_t ph[3] = {0, 0, 0};  // diagnostic: of which inputs, filters, write-out issue (the rest: drain)
-#endif
 };
 
 // Are chunk st.k's inputs present (row r-1's progress, this row's granules)?
@@ -1672,15 +1428,9 @@ __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState&
   // Row r-1's progress and the info granule of the chunk's last macroblock
   // (stored last; the row is coded left to right), both loads issued before
   // either is tested: one fabric round trip, not two.
-#if CAIRO_READY_PAIR
   const uint64_t p = r > 0 ? progress_at(&a.progress[r - 1]) : ~0ull;
   const uint64_t g = gran_ld(gran_mb(a, (c1 - 1) >> 4, r) + kGranulesPerMB);
   return (p >= tagged(a.epoch, c1)) & ((uint32_t)(g >> 32) == a.epoch);
-#else
-  if (r > 0 && progress_at(&a.progress[r - 1]) < tagged(a.epoch, c1)) return false;
-  const uint64_t g = gran_ld(gran_mb(a, (c1 - 1) >> 4, r) + kGranulesPerMB);
-  return (uint32_t)(g >> 32) == a.epoch;
-#endif
 }
 
 // Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs, or
@@ -1759,7 +1509,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           // every load of this lane issued before the first LDS store: one
           // fabric round trip, not one per load (nall <= 256 dwords over >= 56
           // lanes: at most kAbove each)
-          constexpr int kAbove = CAIRO_ABOVE_BATCH ? (8 << (6 - 1)) / (64 - 2 * kDbMBs) + 1 : 1;
+          constexpr int kAbove = (8 << (6 - 1)) / (64 - 2 * kDbMBs) + 1;
           uint32_t v[kAbove];
           int16_t* dst[kAbove];
           for (int i0 = t3 - 2 * nmb; i0 < nall; i0 += kAbove * (64 - 2 * nmb)) {  // one pass when batched
@@ -1796,16 +1546,14 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
       }
     }
     __syncthreads();
-    const uint64_t t1 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---- the filters, in four dependent phases (band A H edges, band A V
     //      edges, band B H, band B V); the lines of one phase are disjoint.
-    //      64-column chunks (4K) spread each phase over the four waves with a
-    //      workgroup barrier between phases; narrower chunks have at most 64
-    //      lines per phase and stay in wave 0, whose LDS accesses execute in
-    //      order (no workgroup barrier) ----
+    //      All in wave 0, whose LDS accesses execute in order (no workgroup
+    //      barrier between the phases; spreading a 64-column chunk's phases
+    //      over the four waves with barriers was 0.3 % slower at 4K,
+    //      profiles/r04/ab_4k_s.txt, ab_4k_t.txt) ----
     {
-      const bool spread = kDbSpread && a.db_shift >= 6;  // workgroup-uniform
-      const int nthr = spread ? 256 : 64;
+      constexpr int nthr = 64;
       const bool part = tid < nthr;
       const int ls = a.db_shift, kL = 1 << ls, kC = kL >> 1;  // luma / chroma columns of a whole chunk
       // band A H edges of [c0, c1): luma kL columns, then chroma 2 x kC
@@ -1819,7 +1567,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
             db_line(D, pl, true, 0, col, D.info[0][(col >> 3) & 7], D.info[1][(col >> 3) & 7]);
         }
       }
-      if (spread) __syncthreads(); else __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_wave_barrier();
       // band A V edges of the luma units c0, c0+8, ... and the chroma units c0/2, c0/2+8, ...
       for (int i = tid; part && i < kL + 2 * kC; i += nthr) {
         if (i < kL) {
@@ -1832,18 +1580,17 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
             db_line(D, pl, false, row, x - 4, D.info[1][((x - 1) >> 3) & 7], D.info[1][(x >> 3) & 7]);
         }
       }
-      if (spread) __syncthreads(); else __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_wave_barrier();
       // band B H edges of [hb0, hb1), then V edges of units [vb0, vb1)
       for (int col = hb0 + tid; part && col < hb1; col += nthr)
         db_line(D, 0, true, 8, col, D.info[1][(col >> 4) & 7], D.info[1][(col >> 4) & 7]);
-      if (spread) __syncthreads(); else __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_wave_barrier();
       for (int i = tid; part && i < 8 * ((vb1 - vb0 + 7) >> 3); i += nthr) {
         const int x = vb0 + 8 * (i >> 3), row = 12 + (i & 7);
         if (x < vb1) db_line(D, 0, false, row, x - 4, D.info[1][((x - 1) >> 4) & 7], D.info[1][(x >> 4) & 7]);
       }
     }
     __syncthreads();
-    const uint64_t t2 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
     hb0 = max(hb0, hb1);
     vb0 = max(vb0, vb1);
     const int w1 = last ? a.wa : max(w0, c1 - 12);
@@ -1879,14 +1626,8 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(pick(planes(a.push[q]), pl) + off), d,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      const uint64_t t3 = tb ? __builtin_amdgcn_s_memrealtime() : 0;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-#if CAIRO_DB_PHASES
-      if (tb) st.ph[0] += t1 - tb, st.ph[1] += t2 - t1, st.ph[2] += t3 - t2;
-#else
-      (void)t1, (void)t2, (void)t3;
-#endif
       if (tid == 0) {
         if (a.sys) {  // the next frame may read this row from another device
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -1927,17 +1668,13 @@ __device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& s
 // order equals signed order (reconstructions are unclamped int16, SURVEY.md
 // Appendix A.4), which lets the candidate search use packed u16 instructions.
 // Columns are circular (x & 127, chroma x & 63); the first 16 (4) columns are
-// repeated after the last so that a row read never wraps.  Pitches: 74 / 37
-// dwords, so the 16 rows a candidate group reads hit 16 distinct banks.
-// Luma pitch (elements): 128 + 16-column tail + pad.  Only 2- and 4-byte
-// accesses touch this window, so the pitch is free: an odd number of dwords
-// (150 elements = 75) puts the 16 rows of a candidate's lane group on 16
-// distinct banks of either parity, so the wave's other groups (offsets of a
-// search step) do not all land on the same 16 even banks (148 = 74 dwords).
-#ifndef CAIRO_CW_PITCH
-#define CAIRO_CW_PITCH 150
-#endif
-constexpr int kCwLP = CAIRO_CW_PITCH;
+// repeated after the last so that a row read never wraps.  Luma pitch
+// (elements): 128 + 16-column tail + pad.  Only 2- and 4-byte accesses touch
+// this window, so the pitch is free: an odd number of dwords (150 elements =
+// 75) puts the 16 rows of a candidate's lane group on 16 distinct banks of
+// either parity, so the wave's other groups (offsets of a search step) do not
+// all land on the same 16 even banks (148 = 74 dwords).
+constexpr int kCwLP = 150;
 static_assert(kCwLP % 2 == 0 && kCwLP >= 144, "coder window rows: dword pairs, 128 + 16-column tail");
 constexpr int kCwCP = 74;   // chroma pitch: 64 + 4-column tail + pad
 constexpr int kLumaTail = 16, kChromaTail = 4;
@@ -1948,35 +1685,37 @@ struct alignas(16) RowWindow {
   int16_t v[40 * kCwCP];
 };
 
-// The row coder's source macroblocks through LDS: wave 0 stages macroblock
-// bx+1's source (src_dma) while bx is coded, so neither the source rows at a
-// macroblock's start nor the residual's source elements after its search
-// cost a fabric round trip.  1: issued at the macroblock's start, with the
-// fresh granule load (an LDS-DMA in flight makes the compiler drain vmcnt at
-// the next barrier or global-load use: hipcc, ROCm 7.2), 2: just before the
-// macroblock's final drain.  0: both read from the planes.
-#ifndef CAIRO_SRC_DMA
-#define CAIRO_SRC_DMA 1
-#endif
-constexpr int kSrcDma = CAIRO_SRC_DMA;
-
-// The 16 lane groups of the workgroup cover a stage's 9 candidates; groups
-// 9..15 (the top of wave 2 and all of wave 3) idle instead of repeating
-// candidate 8 (0): 7/16 of the stage's LDS reads and VALU work saved.
-#ifndef CAIRO_INTRA_IDLE
-#define CAIRO_INTRA_IDLE 1
-#endif
-constexpr bool kIntraIdle = CAIRO_INTRA_IDLE;
-
+// The row coder's source macroblocks go through LDS: wave 0 stages
+// macroblock bx+1's source (src_dma) at bx's start, with the fresh granule
+// load (an LDS-DMA in flight makes the compiler drain vmcnt at the next
+// barrier or global-load use: hipcc, ROCm 7.2), so neither the source rows at
+// a macroblock's start nor the residual's source elements after its search
+// cost a fabric round trip.
 constexpr int kWaitVm0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+
 // A macroblock's end waits only for its coefficient stores (which its info
 // granule releases to the deblock and, through its progress, to the next
 // frame's copy macroblocks), not for the pixel-granule and table stores
-// issued after them (1), or for everything (0).
-#ifndef CAIRO_COEF_DRAIN
-#define CAIRO_COEF_DRAIN 1
-#endif
-constexpr bool kCoefDrain = CAIRO_COEF_DRAIN;
+// issued after them: vmcnt retires in order, so wave w waits until no more
+// than the stores it issued after its last coefficient store are
+// outstanding.  Those are, in program order (compiler barriers keep it):
+// one pixel-granule store per 8x8 block the wave owns (blocks w and w+4:
+// two for waves 0 and 1, one for waves 2 and 3), then, on wave 0, the
+// 16-byte block-table store.
+constexpr int kBlocksOfWave[4] = {2, 2, 1, 1};
+// s_waitcnt vmcnt(N) (N < 16: gfx9 encoding, expcnt and lgkmcnt left free),
+// also a compiler barrier.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 16, "vmcnt immediate");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+  asm volatile("" ::: "memory");
+}
+constexpr int kStoresAfterCoef[4] = {kBlocksOfWave[0] + 1, kBlocksOfWave[1], kBlocksOfWave[2], kBlocksOfWave[3]};
+static_assert(kStoresAfterCoef[0] == 3 && kStoresAfterCoef[1] == 2 && kStoresAfterCoef[2] == 1 &&
+                  kStoresAfterCoef[3] == 1,
+              "the s_waitcnt immediates in code_row");
 
 
 struct alignas(16) RowLds {
@@ -1985,68 +1724,7 @@ struct alignas(16) RowLds {
   int16_t bufA[kMBElems], bufB[kMBElems];  // per-block transform scratch, block-major
   int32_t cand[2][16][2];                  // double-buffered candidate (sad, mad)
   int32_t red[12];
-#if CAIRO_CODER_DEBLOCK
-  DbLds db;  // the row's deblock tile
-#endif
 };
-
-// The row coder's first load of the row above's fresh granules before its
-// group-start wait (1) or after it (0).
-#ifndef CAIRO_EARLY_GRAN
-#define CAIRO_EARLY_GRAN 1
-#endif
-constexpr bool kEarlyGran = CAIRO_EARLY_GRAN;
-// At a group start, the intra search before the wait for the group's inter
-// records (1) or after it (0).
-#ifndef CAIRO_SEARCH_FIRST
-#define CAIRO_SEARCH_FIRST 1
-#endif
-constexpr bool kSearchFirst = CAIRO_SEARCH_FIRST;
-
-// Deblock chunks the coder may leave pending at a group start before it runs
-// a ready one even when its inter records are already there (the next
-// frame's helpers wait for this row's progress).
-#ifndef CAIRO_CODER_DB_LAG
-#define CAIRO_CODER_DB_LAG 3
-#endif
-constexpr int kCoderDbLag = CAIRO_CODER_DB_LAG;
-
-// Row coder at the start of group g (MB bx = 4g): until the group's nref inter
-// records are in (inter_done), running this row's ready deblock chunks
-// meanwhile -- and a ready one anyway while more than kCoderDbLag chunks are
-// pending.  Only ready chunks run here (their inputs: this row's coded
-// macroblocks, the row above's progress), so the coder never blocks on a
-// deblock; bounded like every wait.
-template <int kDummy = 0>
-__device__ __forceinline__ void coder_wait(FA& a, int by, int bx, DbLds& D, DbState& st, int* flag) {
-  volatile int* vflag = flag;
-  int32_t* word = &a.inter_done[by * a.ng + (bx >> 2)];
-  uint64_t t0 = 0;
-  for (;;) {
-    int d = 0;
-    if (threadIdx.x == 0) {
-      const int nrec = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool can = ((st.k + 1) << (a.db_shift - 4)) <= bx && deblock_chunk_ready(a, by, st);
-      const bool recs = nrec >= a.nref;
-      if (can && (!recs || (bx >> (a.db_shift - 4)) - st.k > kCoderDbLag)) {
-        d = 2;
-      } else if (recs || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        d = 1;
-      } else {
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (!t0) t0 = now;
-        __builtin_amdgcn_s_sleep(CAIRO_WAIT_SLEEP);
-        if (now - t0 > 200000000ull) {
-          report_timeout(a, kWaitRecords, by, a.nref, bx >> 2, (uint32_t)nrec);
-          d = 1;
-        }
-      }
-    }
-    d = wg_broadcast(vflag, d);
-    if (d == 1) break;
-    if (d == 2) deblock_chunk(a, by, D, st, true);
-  }
-}
 
 // Pixel pair (int16 lo = column col, hi = col+1; col even) of plane pl at
 // window row `row`.
@@ -2125,20 +1803,11 @@ __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int
 
 // lerp_px on both halves of two biased u16 pairs; the result as a biased pair.
 // On the biased halves directly (lerp_half_bb).
-#ifndef CAIRO_LERP_PAIR_B
-#define CAIRO_LERP_PAIR_B 1
-#endif
 __device__ __forceinline__ uint32_t lerp_pair(uint32_t pa, uint32_t pb, int q) {
-  if (CAIRO_LERP_PAIR_B) {
-    const uint32_t a0 = pa & 0xFFFFu, b0 = pb & 0xFFFFu, a1 = pa >> 16, b1 = pb >> 16;
-    const uint32_t l0 = q ? lerp_quarter_bb(a0, b0) : lerp_half_bb(a0, b0);
-    const uint32_t l1 = q ? lerp_quarter_bb(a1, b1) : lerp_half_bb(a1, b1);
-    return l0 | (l1 << 16);
-  }
-  const uint32_t ua = pa ^ 0x80008000u, ub = pb ^ 0x80008000u;
-  const int l0 = lerp_px((int16_t)ua, (int16_t)ub, q);
-  const int l1 = lerp_px((int16_t)(ua >> 16), (int16_t)(ub >> 16), q);
-  return (((uint32_t)l0 & 0xFFFFu) | ((uint32_t)l1 << 16)) ^ 0x80008000u;
+  const uint32_t a0 = pa & 0xFFFFu, b0 = pb & 0xFFFFu, a1 = pa >> 16, b1 = pb >> 16;
+  const uint32_t l0 = q ? lerp_quarter_bb(a0, b0) : lerp_half_bb(a0, b0);
+  const uint32_t l1 = q ? lerp_quarter_bb(a1, b1) : lerp_half_bb(a1, b1);
+  return l0 | (l1 << 16);
 }
 
 // Sub-pel candidate: lerp of the best block (bx, by) toward neighbour (tx, ty),
@@ -2288,12 +1957,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
   const int cw = a.wa >> 1;
   const int nblk = wave < 2 ? 2 : 1;  // wave w owns 8x8 blocks w and w+4
   const int mbs = a.wmb * a.hmb;
-#if CAIRO_CODER_DEBLOCK
-  DbState dst{0, 0, 0, 8};
-#endif
   {
     const int py = by * kMB, oy = py - 48;
-    if (kSrcDma && !kDecode) {  // macroblock 0's source; later ones are staged a macroblock ahead
+    if (!kDecode) {  // macroblock 0's source; later ones are staged a macroblock ahead
       src_dma(a, 0, by, L.src[0]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -2310,10 +1976,10 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // 64-bit load needs no acquire).
       // macroblock bx+1's source into LDS, in flight with the fresh granule
       // load below, whose wait covers it (the buffer was last read in bx-1)
-      if (kSrcDma == 1 && !kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
+      if (!kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
       const bool fresh_col = by > 0 && bx != 0 && bx + 2 < a.wmb && tid < kGranulesPerMB;
       const uint64_t* fresh_gp = fresh_col ? gran_at(a, bx + 2, by - 1, tid) : nullptr;
-      const uint64_t fresh_g = (kEarlyGran && fresh_col) ? gran_ld(fresh_gp) : 0;
+      const uint64_t fresh_g = fresh_col ? gran_ld(fresh_gp) : 0;
       // At a group start the coder needs the group's inter records, and every
       // cross-frame dependency they carry (the stale rows, references and
       // previous output_cache), only for the classification: the intra search
@@ -2321,7 +1987,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // records may still be on their way; the acquire, when the records are
       // already in, completes behind it (it issues no vector-memory access).
       const bool gstart = (bx & 3) == 0;
-      const bool early = kSearchFirst && !kDecode && !kCoderDeblock && gstart;  // workgroup-uniform
+      const bool early = !kDecode && gstart;  // workgroup-uniform
       uint64_t tacc = acct_now();
       // thread 0: one poll of the group's record count, issued with the fresh
       // granule load and tested after the window update (which waits for it anyway)
@@ -2329,7 +1995,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // macroblock's record of reference 1 -- the helper's last search, after
       // its wait for the previous frame -- carries this frame's tag; otherwise
       // (intra and decoded frames: the helper's carrier) once inter_done says so.
-      const bool by_tag = kTaggedRecords && a.inter;  // workgroup-uniform
+      const bool by_tag = a.inter;  // workgroup-uniform
       const uint64_t* grec = (const uint64_t*)&a.inter_desc[mb];  // reference 1, this MB
       uint64_t rd0 = 0;
       if (early && tid == 0)
@@ -2338,14 +2004,10 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
                                                    __HIP_MEMORY_SCOPE_AGENT);
       bool ready0 = false;  // thread 0: the records were in before the search
       if (gstart && !early) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
-#if CAIRO_CODER_DEBLOCK
-        coder_wait(a, by, bx, L.db, dst, flag);
-#else
         if (tid == 0) {
           if (by_tag) rec_settle(a, grec, gran_ld(grec), by, mb);
           else wait_records(a, by, bx >> 2);
         }
-#endif
         acquire_after_wait(a.sys);  // the stale rows, references and previous output_cache
         acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
       }
@@ -2370,21 +2032,21 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           }
         } else if (fresh_col) {
           win_put_k(L.win, oy, bx + 2, by - 1, tid,
-                    gran_settle(a, fresh_gp, kEarlyGran ? fresh_g : gran_ld(fresh_gp), by));
+                    gran_settle(a, fresh_gp, fresh_g, by));
         }
       }
       acct_add(a.acct, Acct::kCoderWindow, acct_now() - tacc);
       // the source DMA has landed (free where the granule wait above covered
       // it): a wait the compiler sees, so it knows no LDS-DMA is in flight and
       // the barrier before the search does not drain the loads issued below
-      if (kSrcDma == 1 && !kDecode) __builtin_amdgcn_s_waitcnt(kWaitVm0);
+      if (!kDecode) __builtin_amdgcn_s_waitcnt(kWaitVm0);
       if (early && tid == 0) {
         ready0 = by_tag ? (uint32_t)(rd0 >> 32) == a.epoch : (int)rd0 >= a.nref;
         if (ready0) acquire_fence(a.sys);  // completes during the search; waited for after it
       }
       // source rows of this lane's group slot
       SrcRow s;  // biased u16 pairs (the encoder's source; unused when decoding)
-      if (!kDecode && kSrcDma) {
+      if (!kDecode) {
         // staged in LDS during macroblock bx-1 (landed behind its final drain
         // and barrier; at bx == 0 behind the row start's)
         const uint32_t* m = (const uint32_t*)L.src[bx & 1];
@@ -2393,18 +2055,6 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         const int co = (gi >> 1) * 4 + (gi & 1) * 2;
         s.u[0] = m[128 + co] ^ 0x80008000u, s.u[1] = m[128 + co + 1] ^ 0x80008000u;
         s.v[0] = m[160 + co] ^ 0x80008000u, s.v[1] = m[160 + co + 1] ^ 0x80008000u;
-      } else if (!kDecode) {
-        const uint4* ry = (const uint4*)(a.in.y + (size_t)(py + gi) * a.wa + px);
-        const uint4 r0 = ry[0], r1 = ry[1];
-        s.y[0] = r0.x, s.y[1] = r0.y, s.y[2] = r0.z, s.y[3] = r0.w;
-        s.y[4] = r1.x, s.y[5] = r1.y, s.y[6] = r1.z, s.y[7] = r1.w;
-        const size_t co = (size_t)((py >> 1) + (gi >> 1)) * cw + (px >> 1) + (gi & 1) * 4;
-        const uint2 u2 = *(const uint2*)(a.in.u + co), v2 = *(const uint2*)(a.in.v + co);
-        s.u[0] = u2.x, s.u[1] = u2.y, s.v[0] = v2.x, s.v[1] = v2.y;
-#pragma unroll
-        for (int k = 0; k < 8; k++) s.y[k] ^= 0x80008000u;
-#pragma unroll
-        for (int k = 0; k < 2; k++) s.u[k] ^= 0x80008000u, s.v[k] ^= 0x80008000u;
       }
       const bool pf3 = by >= 3 && bx + 3 < a.wmb, pf2 = by >= 2 && bx + 3 < a.wmb;
       const bool pfs = by + 1 < a.hmb && bx + 1 < a.wmb;
@@ -2422,39 +2072,22 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       int ipv[kMaxRing - 1][2];
       const int nref = a.inter ? a.ring - 1 : 0;
       auto load_inter = [&]() {
-        if (kTaggedRecords) {
-          // each wave loads the macroblock's 2 * nref record granules (every
-          // lane the same addresses), all issued before the first is tested
-          uint64_t rg[kMaxRing - 1][2];
+        // each wave loads the macroblock's 2 * nref record granules (every
+        // lane the same addresses), all issued before the first is tested
+        uint64_t rg[kMaxRing - 1][2];
 #pragma unroll
-          for (int o = 0; o < kMaxRing - 1; o++) {
-            if (o >= nref) break;
-            const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
-            rg[o][0] = gran_ld(r);
-            rg[o][1] = gran_ld(r + 1);
-          }
+        for (int o = 0; o < kMaxRing - 1; o++) {
+          if (o >= nref) break;
+          const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
+          rg[o][0] = gran_ld(r);
+          rg[o][1] = gran_ld(r + 1);
+        }
 #pragma unroll
-          for (int o = 0; o < kMaxRing - 1; o++) {
-            if (o >= nref) break;
-            const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
-            inter_d[o] = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
-            inter_sad[o] = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
-          }
-        } else {
-          uint4 idw[kMaxRing - 1];  // all records' loads issued before the first wait
-          int isw[kMaxRing - 1];
-#pragma unroll
-          for (int o = 0; o < kMaxRing - 1; o++) {
-            if (o >= nref) break;
-            idw[o] = *(const uint4*)&a.inter_desc[o * mbs + mb];
-            isw[o] = a.inter_sad[o * mbs + mb];
-          }
-#pragma unroll
-          for (int o = 0; o < kMaxRing - 1; o++) {
-            if (o >= nref) break;
-            inter_d[o] = uni_desc_words(idw[o]);
-            inter_sad[o] = uni(isw[o]);
-          }
+        for (int o = 0; o < kMaxRing - 1; o++) {
+          if (o >= nref) break;
+          const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
+          inter_d[o] = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
+          inter_sad[o] = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
         }
 #pragma unroll
         for (int o = 0; o < kMaxRing - 1; o++) {
@@ -2498,7 +2131,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           const int step = stage == 0 ? kRadius : (kRadius >> stage);
           const int jlo = stage == 0 ? -2 * kRadius : -step;
           const int bx0 = sel.bx, by0 = sel.by;
-          if (!kIntraIdle || grp < 9) {  // group g < 9 evaluates candidate g (kIntraIdle: groups 9..15 idle)
+          if (grp < 9) {  // group g < 9 evaluates candidate g; groups 9..15 idle (7/16 of the work saved)
             const int c = min(grp, 8);
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
@@ -2595,17 +2228,11 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // searches: live across them, they pushed the engine into scratch
       // spills
       int svp[2] = {0, 0};
-      if (!kDecode && kSrcDma) {
+      if (!kDecode) {
         _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
           int pl, ex, ey;
           elem_coords((wave + 4 * bi) * 64 + lane, 0, 0, pl, ex, ey);
           svp[bi] = L.src[bx & 1][pl == 0 ? ey * 16 + ex : 256 + (pl - 1) * 64 + ey * 8 + ex];
-        }
-      } else if (!kDecode) {
-        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
-          int pl, ex, ey;
-          elem_coords((wave + 4 * bi) * 64 + lane, px, py, pl, ex, ey);
-          svp[bi] = plane_of(planes(a.in), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
         }
       }
 
@@ -2688,6 +2315,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         }
       }
       stamp(a, mb, 7);
+      asm volatile("" ::: "memory");  // program order: the coefficient stores, then (kStoresAfterCoef) ...
       // publish first (the next row's coder waits for exactly these): pixel
       // pairs (lane, lane^1) of each 8x8 block as granules.  No drain before
       // them: the coefficient stores only have to be visible to whoever
@@ -2722,22 +2350,22 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
                     gran_settle(a, gran_at(a, bx + 3, by - 2, tid), pg2, by));
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
+      asm volatile("" ::: "memory");  // ... the pixel-granule stores, then the table store
       if (tid == 0 && !kDecode) *(uint4*)&a.table[mb] = __builtin_bit_cast(uint4, d);  // one 16-byte store
-      if (kSrcDma == 2 && !kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
       // every wave's coefficient stores drained, then the block info for the
       // deblock (its edge strengths); thread 0's drain covers only wave 0, so
       // the other waves drain before the barrier of the next macroblock --
       // the deblock reads their coefficients only through this granule, hence
       // the barrier: info after all four waves drained
-      if (kCoefDrain && !kDecode) {
-        // only the coefficient stores: after them each wave issued its pixel
-        // granule stores (one per block: wave 0 and 1 two, waves 2 and 3
-        // one) and wave 0 the table store, which need no drain (tag-polled;
-        // read after the launch), and vmcnt retires in order.  More
-        // operations after them (stamps, accounting) only wait longer.
-        if (wave == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else if (wave == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      if (!kDecode) {
+        // only the coefficient stores (kStoresAfterCoef): the pixel-granule
+        // and table stores after them need no drain (tag-polled; read after
+        // the launch).  More vector-memory operations after them (granule
+        // re-polls, stamps) only make the wait longer.
+        if (wave == 0) wait_vmcnt<kStoresAfterCoef[0]>();
+        else if (wave == 1) wait_vmcnt<kStoresAfterCoef[1]>();
+        else if (wave == 2) wait_vmcnt<kStoresAfterCoef[2]>();
+        else wait_vmcnt<kStoresAfterCoef[3]>();
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -2749,11 +2377,6 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
   }
-#if CAIRO_CODER_DEBLOCK
-  // the rest of the row's deblock (each chunk waits for the row above)
-  const int nch = db_chunks(a);
-  while (dst.k < nch) deblock_chunk(a, by, L.db, dst);
-#endif
 }
 
 
@@ -2792,44 +2415,23 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     // progress word, tagged epoch-2, also covers frame index-3: that frame's
     // row r+2 waited for index-3's row r+4 over a wider window), so these
     // searches fill what used to be the wait for the previous frame.
-    if (kGroupSource && a.inter) {
-      if (!kHelperSrcDma) {
-        group_source(a, r, g, L.inter);
-      } else {
-        if (g == 0) {  // the row's first group: staged here and waited for
-          group_source(a, r, 0, L.inter, true);
-          __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        }
-        // group g+1 (into the buffer group g-1 used; each wave reads only its
-        // own macroblock's source, so its own vmcnt waits cover its DMA)
-        if (g + 1 < a.ng) group_source(a, r, g + 1, L.inter, true);
-      }
-    }
+    if (a.inter) group_source(a, r, g, L.inter);
     if (a.inter && a.nref >= 2) {
-      helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag,
-                  kSpecStage ? &L.inter.full : nullptr, inter_need_cols(a, g, 2));
+      helper_wait(a, 2, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
       const uint64_t ts = acct_now();
-      const int full2 = kSpecStage ? L.inter.full : -1;  // (written before helper_wait's barriers)
-      if (kSpecStage)  // reference 2's window in flight with the zero-MV loads of references 2..R-1
-        dma_window(L.inter.win, RECON_AT(a, 2), a.wa, a.ha, 4 * g * kMB - 32, r * kMB - 32, 0,
-                   full2 ? kWinL : kLvl1Rows, 0, full2 ? kWinLW : kLvl1Cols);
-      if (kGroupSource) zero_mv_older(a, r, g, L.inter);
-      for (int off = 2; off <= a.nref; off++)
-        inter_task(a, r, g, off, L.inter, L.db, st, flag, is, 0, full2, kSpecStage && off == 2);
+      zero_mv_older(a, r, g, L.inter);
+      for (int off = 2; off <= a.nref; off++) inter_task(a, r, g, off, L.inter, L.db, st, flag, is);
       acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
     }
     // level 1 of the group's window in the previous frame; deblock meanwhile
-    // (a deblock chunk started here delays the search when the previous
-    // frame's progress arrives meanwhile: CAIRO_DB_IN_WAIT1 = 0 leaves the
-    // chunks to the catch-up after the group's records)
-    helper_wait<CAIRO_DB_IN_WAIT1 != 0>(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag,
-                                        kSpecStage && a.inter ? &L.inter.full : nullptr, inter_need_cols(a, g, 2));
+    // (leaving the chunks to the catch-up after the group's records instead
+    // measured neutral)
+    helper_wait(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
     if (a.inter) {
       const uint64_t ts = acct_now();
-      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is, a.nref,  // publishes the group's nref records
-                 kSpecStage ? L.inter.full : -1);
+      inter_task(a, r, g, 1, L.inter, L.db, st, flag, is);
       acct_add(a.acct, Acct::kHelperSearch, acct_now() - ts);
     } else if (tid == 0) {  // intra frame: carry the dependency only
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -2840,9 +2442,9 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     int caught = 0;
     const uint64_t tc = acct_now();
     uint64_t tcdb = 0;
-    for (; !kCoderDeblock;) {  // catch the deblock up with what has arrived
+    for (;;) {  // catch the deblock up with what has arrived
       int d = 0;
-      if (tid == 0) d = !kCoderDeblock && kHelperInterleave && st.k < nch && deblock_chunk_ready(a, r, st);
+      if (tid == 0) d = st.k < nch && deblock_chunk_ready(a, r, st);
       if (!wg_broadcast(vflag, d)) break;
       const uint64_t tb = acct_now();
       deblock_chunk(a, r, L.db, st, true);
@@ -2853,7 +2455,7 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
     if (is) is[11] = ((uint64_t)caught << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - is[2]);
   }
   trace(tr, 1, 1000);
-  while (!kCoderDeblock && st.k < nch) {
+  while (st.k < nch) {
     trace(tr, 3, 60000 + st.k);
     deblock_chunk(a, r, L.db, st);
   }
@@ -2861,9 +2463,6 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
   if (a.stamps && tid == 0) {  // the row's deblock times, in per-row stamp slots no chunk uses at these widths
     uint64_t* ds = a.stamps + (size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps;
     ds[kDbStamps - 1] = st.busy;
-#if CAIRO_DB_PHASES
-    ds[kDbStamps - 2] = st.ph[0], ds[kDbStamps - 3] = st.ph[1], ds[kDbStamps - 4] = st.ph[2];
-#endif
   }
 }
 
@@ -2887,13 +2486,8 @@ __device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag
 // deadlock with every workgroup resident.
 // ---------------------------------------------------------------------------
 
-#ifndef CAIRO_PRIO_FRAME_MBS
-#define CAIRO_PRIO_FRAME_MBS 4000
-#endif
-constexpr int kPrioFrameMBs = CAIRO_PRIO_FRAME_MBS;  // helpers get issue priority above this frame size
-#ifndef CAIRO_PRIO_LEVEL
-#define CAIRO_PRIO_LEVEL 2
-#endif
+constexpr int kPrioFrameMBs = 4000;  // helpers get issue priority above this frame size
+constexpr int kPrioLevel = 2;        // (1 and 3 measured the same)
 
 // Pool of workgroup b out of n, nh of them helpers: spread evenly over the
 // block indices (so over every XCD, which take blocks round-robin), and a
@@ -2915,15 +2509,9 @@ __device__ __forceinline__ bool is_helper(int b, int nh, int n) {
 // task always has a free worker: its label's workers hold only
 // finished tasks.  Returns the task's index in its order (prev: the previous
 // launch's), or -1 when every queue is exhausted.
-#ifndef CAIRO_SHARE
-#define CAIRO_SHARE 1
-#endif
-#ifndef CAIRO_STEAL
-#define CAIRO_STEAL 2
-#endif
-constexpr int kSteal = CAIRO_STEAL;
+constexpr int kSteal = 2;
 __device__ __forceinline__ int next_task(const EngineArgs& e, int pool, int lab, EngineLds& L, bool& prev) {
-  const int ptotal = CAIRO_SHARE ? e.ptotal : 0;
+  const int ptotal = e.ptotal;
   if (threadIdx.x < 64) {  // wave 0; lane l < nlab looks after label l
     const int l = threadIdx.x, nlab = e.nlab[pool];
     const bool act = l < nlab;
@@ -2991,12 +2579,9 @@ __device__ __forceinline__ int next_task(const EngineArgs& e, int pool, int lab,
 // (the first to arrive proposes XCC_ID - b, i.e. the offset that makes a
 // label an XCD when blocks are dealt round-robin) so labels stay a
 // partition of the classes whatever the placement.
-#ifndef CAIRO_CLASS_SPLIT
-#define CAIRO_CLASS_SPLIT 0
-#endif
 __device__ __forceinline__ int worker_label(const EngineArgs& e, int b, bool& helper, EngineLds& L) {
   const int n = e.n_helpers + e.n_rows;
-  if (e.nlab[0] == 1 && e.nlab[1] == 1 && !(CAIRO_CLASS_SPLIT && n % kLabels == 0 && e.n_helpers % kLabels == 0)) {
+  if (e.nlab[0] == 1 && e.nlab[1] == 1) {
     helper = is_helper(b, e.n_helpers, n);
     return 0;
   }
@@ -3042,7 +2627,7 @@ __global__ __launch_bounds__(256, 3) void k_engine(EngineArgs e) {
     // The helpers' inter records gate every row coder at its group starts:
     // on large frames they win the SIMD issue arbitration against the coders'
     // waves (A/B: 1080p +3 %, 4K +3 %; 720p -1 %, so not there).
-    if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(CAIRO_PRIO_LEVEL);
+    if (e.wmb * e.hmb > kPrioFrameMBs) __builtin_amdgcn_s_setprio(kPrioLevel);
     for (;;) {
       bool prev;
       const uint64_t tq = acct_now();
@@ -3117,7 +2702,6 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   const size_t mbs = (size_t)e.wmb * e.hmb, nref = e.ring > 1 ? e.ring - 1 : 1;
   a.table = e.table_base + (size_t)f.slot * mbs;
   a.inter_desc = e.idesc_base + (size_t)f.slot * nref * mbs;
-  a.inter_sad = e.isad_base + (size_t)f.slot * nref * mbs;
   a.granules = e.gran_base + (size_t)f.slot * mbs * kGranuleStride;
   a.err = e.sync + SyncLayout::kErr;
   a.sticky = e.sticky;
@@ -3138,7 +2722,7 @@ FrameArgs make_frame_view(const EngineArgs& e, const FrameDesc& f, int j) {
   // frames feel the latter more (A/B, Mpix/s, chunk 16 / 32 / 64: 720p
   // 3859-3870 / 3384-3435 / 2893-2916, 1080p 4549 / 4660 / 4133, 4K 4784 /
   // 4940 / 5040)
-  a.db_shift = CAIRO_DB_CHUNK ? __builtin_ctz(CAIRO_DB_CHUNK) : (e.wmb >= 200 ? 6 : e.wmb >= 100 ? 5 : 4);
+  a.db_shift = e.wmb >= 200 ? 6 : e.wmb >= 100 ? 5 : 4;
   a.stamps = e.stamps ? e.stamps + (size_t)j * stamp_frame_words(e.wmb, e.hmb) : nullptr;
   a.acct = e.acct;
   {

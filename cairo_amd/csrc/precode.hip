@@ -392,9 +392,21 @@ __global__ __launch_bounds__(256) void k_feed_copy(FeedArgs f) {
     const uint4* tb = (const uint4*)((FA*)f.fa)[j].table;
     for (uint64_t i = i0; i < (uint64_t)f.table_words; i += di) th[i] = tb[i];
   }
-  if (f.err_host[j] && blockIdx.x == 0 && threadIdx.x < TimeoutInfo::kWords)
-    f.err_host[j][threadIdx.x] = __hip_atomic_load(((FA*)f.fa)[j].sticky + threadIdx.x, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
+  if (f.err_host[j] && blockIdx.x == 0 && threadIdx.x < 64) {
+    // the timeout record: its kind first (acquire: it is stored last, with
+    // release, kernels.hip report_timeout), then the payload -- a record
+    // seen complete, or no record
+    const int32_t* sticky = ((FA*)f.fa)[j].sticky;
+    const int32_t kind = __shfl(
+        threadIdx.x == 0 ? __hip_atomic_load(sticky + TimeoutInfo::kKind, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0,
+        0);
+    if (threadIdx.x < TimeoutInfo::kWords)
+      f.err_host[j][threadIdx.x] =
+          threadIdx.x == TimeoutInfo::kKind
+              ? kind
+              : (kind ? __hip_atomic_load(sticky + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0);
+  }
 }
 
 }  // namespace

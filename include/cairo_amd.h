@@ -32,6 +32,16 @@ extern "C" {
 
 #define CAIRO_API __attribute__((visibility("default")))
 
+/* Version of this C ABI.  It is bumped whenever an exported entry point
+ * changes its signature or meaning; a caller built against one header checks
+ * cairo_api_version() == CAIRO_AMD_API_VERSION at start-up.
+ *   1  round 3: cairo_task_queues(hmb, frames, pool, ...)
+ *   2  round 4: cairo_task_queues gains n_helpers and n_rows,
+ *      cairo_group_check_queues gains hw_queues
+ *   3  round 5: cairo_ctx_read_inter refuses stale (untagged) records */
+#define CAIRO_AMD_API_VERSION 3
+CAIRO_API int cairo_api_version(void);
+
 typedef struct cairo_ctx cairo_ctx;
 
 /* Outputs a context hands to the host entropy stage (cairo_ctx_set_outputs). */

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Fabric-read attribution of the engine (run on the GPU box from the repo
 # root): each diagnostic build scratch/attr/<name>.so (tools/build_variant.sh
-# with -DCAIRO_ATTR_SKIP=..., kernels.hip) is copied over the in-tree library
+# with -DCAIRO_TOOLS_BUILD -DCAIRO_ATTR_SKIP=..., kernels.hip) is copied over the in-tree library
 # in turn and bench.py runs under ONE --pmc pass of sized read requests and
 # write requests; tools/attr_summary.py then turns the per-build differences
 # into bytes per frame.  The in-tree library is put back however the runs end.

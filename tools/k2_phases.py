@@ -109,11 +109,6 @@ if ok.any():
     if wb <= 255:  # the row's helper deblock time (last per-row stamp slot)
         dbt = dbs[..., 255] / 100.0
         print(f"  helper deblock per row {dbt.mean():.1f} us = {dbt.mean() / max(1, ist.shape[2]):.1f} us per group")
-        ng_ = max(1, ist.shape[2])
-        ph = [dbs[..., 254 - k].mean() / 100.0 / ng_ for k in range(3)]
-        if sum(ph) > 0:  # a build with CAIRO_DB_PHASES=1
-          print(f"    per group: inputs {ph[0]:.1f}, filters {ph[1]:.1f}, write-out issue {ph[2]:.1f}, "
-                f"drain + publish {dbt.mean() / ng_ - sum(ph):.1f} us")
     cu = ist[..., 11][ok]
     print(f"  after each group: deblock catch-up {np.mean(cu & 0xFFFFFFFF) / 100.0:.1f} us, "
           f"{np.mean(cu >> 32):.2f} chunks (of {(wb * 16 + a.db_chunk - 1) // a.db_chunk / max(1, ist.shape[2]):.2f} per group)")
