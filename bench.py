@@ -224,9 +224,8 @@ def frame_hashes(cairo_amd, store: FrameStore, w, h, ring, q, threads: int) -> d
 
 def golden_stream(config: str, content: str, q: int, ring: int):
     """The oracle's per-frame record hashes of this stream, or None."""
-    if content != "band4":
-        return None
-    path = os.path.join(ROOT, "tests", "golden", f"stream_{config}_q{q}_r{ring}.json")
+    sfx = "" if content == "band4" else f"_{content}"
+    path = os.path.join(ROOT, "tests", "golden", f"stream_{config}_q{q}_r{ring}{sfx}.json")
     if not os.path.exists(path):
         return None
     g = json.load(open(path))
@@ -515,7 +514,8 @@ def main():
                 "avg_launch_ms is the per-launch duration rocprofv3 --stats reports)",
     }
     roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 6)
-    pmc_path = a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
+    pmc_path = a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.config}" +
+                                     ("" if a.content == "band4" else f"_{a.content}") + ".json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
         k = pmc.get("per_frame_hbm_bytes_sized") or pmc.get("per_frame_hbm_bytes", {}).get("engine")
@@ -532,7 +532,7 @@ def main():
     ops_path = os.path.join(ROOT, "profiles", "algorithmic_ops.json")
     valu = None
     if os.path.exists(ops_path):
-        ops = json.load(open(ops_path)).get(a.config)
+        ops = json.load(open(ops_path)).get(a.config if a.content == "band4" else f"{a.config}_{a.content}")
         if ops:
             per_frame = ops["pixel_ops_per_p_frame"]
             ach = per_frame / (engine_busy_ms * 1e-3)

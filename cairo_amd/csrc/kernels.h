@@ -112,7 +112,7 @@ enum TimeoutKind : int32_t {
 #ifndef CAIRO_ACCT
 #define CAIRO_ACCT 0
 #endif
-constexpr int kAcctShards = 64, kAcctWords = 24;
+constexpr int kAcctShards = 64, kAcctWords = 32;
 struct Acct {
   // row coders
   static constexpr int kCoderTasks = 0, kCoderTotal = 1, kCoderGroupWait = 2, kCoderWindow = 3, kCoderSearch = 4,
@@ -123,6 +123,10 @@ struct Acct {
   // traffic of the staging and the polls (bytes requested, nominal)
   static constexpr int kWinBytes = 16, kWinSpecUnused = 17, kZeroMvBytes = 18, kGranPollBytes = 19,
                        kRecPollBytes = 20, kWinStages = 21, kSearchedTasks = 22, kInterTasks = 23;
+  // row coders, after the searches: residual .. reconstruction (classify
+  // excluded), publish (granule stores, window update, table), drain (the
+  // coefficient drain, the barrier, the info granule)
+  static constexpr int kCoderXform = 24, kCoderPublish = 25, kCoderDrain = 26;
 };
 
 // Frames per engine launch.

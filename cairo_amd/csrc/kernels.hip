@@ -434,12 +434,17 @@ __device__ __forceinline__ uint4 bias4(uint4 v) {
   return v;
 }
 
-// Traffic attribution builds (tools/attr_traffic.sh; never a product build):
-// bit 0 skips the search-window loads (the windows hold stale LDS), bit 2 the
-// row coder's inter-prediction loads (constant predictions).  The searches and
-// codes then run on wrong data -- same task shapes, wrong results -- so the
-// drop in fabric reads against the default build is what those loads cost.
-// Refused unless the build says it is a tools build.
+// Attribution builds (tools/attr_traffic.sh, tools/attr_valu.sh; never a
+// product build).  Traffic: bit 0 skips the search-window loads (the windows
+// hold stale LDS), bit 2 the row coder's inter-prediction loads (constant
+// predictions); the searches and codes then run on wrong data -- same task
+// shapes, wrong results -- so the drop in fabric reads against the default
+// build is what those loads cost.  Instructions: bit 8 skips the helpers'
+// integer and sub-pel steps (zero-MV records), bit 16 the row coders' intra
+// search (stages and sub-pel), bit 32 the deblock filters; the drop in
+// SQ_INSTS_VALU is what those phases issue (the decisions change too, so the
+// other phases' counts move a little).  Refused unless the build says it is a
+// tools build.
 #ifndef CAIRO_ATTR_SKIP
 #define CAIRO_ATTR_SKIP 0
 #endif
@@ -1006,7 +1011,7 @@ __device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLd
       sad_mad(src, px_from_planes(ref, a.wa, px, py), s.sad, s.mad);
     }
   }
-  const bool need = valid && s.mad >= thr;
+  const bool need = valid && s.mad >= thr && !(CAIRO_ATTR_SKIP & 8);
   if ((threadIdx.x & 63) == 0) L.need[wave] = need;
   if (threadIdx.x == 0) {
     // Is the reference already final over the whole window (level 2 too)?
@@ -1320,7 +1325,7 @@ __device__ __forceinline__ int16_t dequant_elem(int e, int32_t v, int qp, bool i
 __device__ __forceinline__ void dfilter_reg(int* v, int qp, int strength, bool luma) {
   const int p3 = v[0], p2 = v[1], p1 = v[2], p0 = v[3], q0 = v[4], q1 = v[5], q2 = v[6], q3 = v[7];
   const int16_t dpq = (int16_t)iabs(p0 - q0), dp = (int16_t)iabs(p1 - p0), dq = (int16_t)iabs(q1 - q0);
-  if (strength == 0 || dpq >= sAlpha[qp] || dp >= sBeta[qp] || dq >= sBeta[qp]) return;
+  if ((CAIRO_ATTR_SKIP & 32) || strength == 0 || dpq >= sAlpha[qp] || dp >= sBeta[qp] || dq >= sBeta[qp]) return;
   if (strength == 2) {
     v[3] = (int16_t)rdiv(p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1, 8);
     v[2] = (int16_t)rdiv(p2 + p1 + p0 + q0, 4);
@@ -2127,7 +2132,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
         int buf = 0;
   #pragma unroll 1
-        for (int stage = 0; stage < 5; stage++) {
+        for (int stage = 0; stage < ((CAIRO_ATTR_SKIP & 16) ? 0 : 5); stage++) {
           const int step = stage == 0 ? kRadius : (kRadius >> stage);
           const int jlo = stage == 0 ? -2 * kRadius : -step;
           const int bx0 = sel.bx, by0 = sel.by;
@@ -2152,7 +2157,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           buf ^= 1;
         }
         stamp(a, mb, 3);
-        {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
+        if (!(CAIRO_ATTR_SKIP & 16)) {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
           const int bx0 = sel.bx, by0 = sel.by;
           // candidate c = 2 nn + q; q is wave-uniform (waves 0 and 2 the half
           // steps, 1 and 3 the quarter steps), so a wave runs one lerp, not both
@@ -2224,6 +2229,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         }
       }
       stamp(a, mb, 5);
+      const uint64_t tx5 = acct_now();
       // this lane's source elements for the residual, loaded after the
       // searches: live across them, they pushed the engine into scratch
       // spills
@@ -2315,6 +2321,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         }
       }
       stamp(a, mb, 7);
+      const uint64_t tx7 = acct_now();
       asm volatile("" ::: "memory");  // program order: the coefficient stores, then (kStoresAfterCoef) ...
       // publish first (the next row's coder waits for exactly these): pixel
       // pairs (lane, lane^1) of each 8x8 block as granules.  No drain before
@@ -2357,6 +2364,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // the other waves drain before the barrier of the next macroblock --
       // the deblock reads their coefficients only through this granule, hence
       // the barrier: info after all four waves drained
+      const uint64_t tx8 = acct_now();
       if (!kDecode) {
         // only the coefficient stores (kStoresAfterCoef): the pixel-granule
         // and table stores after them need no drain (tag-polled; read after
@@ -2374,6 +2382,12 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         gran_st(gran_at(a, bx, by, kGranulesPerMB),
                 ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index);
       stamp(a, mb, 9);
+      if (CAIRO_ACCT) {
+        const uint64_t tx9 = acct_now();
+        acct_add(a.acct, Acct::kCoderXform, tx7 - tx5);
+        acct_add(a.acct, Acct::kCoderPublish, tx8 - tx7);
+        acct_add(a.acct, Acct::kCoderDrain, tx9 - tx8);
+      }
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
   }

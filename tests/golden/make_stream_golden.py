@@ -9,11 +9,12 @@ every frame the GPU encodes against these without running the oracle on the
 GPU box (about 3.5 s per 4K frame on one core).
 
 The stream is exactly what bench.py submits: frame t is make_band4(w, h, t)
-(seed 1234), frame 0 intra, every later frame a P-frame, quality and ring of
-the config (bench.CONFIGS).  The file is rewritten every `--flush` frames, so
+(seed 1234) -- or bench.content_frame(content, w, h, t) for --content noise /
+static -- frame 0 intra, every later frame a P-frame, quality and ring of the
+config (bench.CONFIGS).  The file is rewritten every `--flush` frames, so
 a partial run leaves a usable prefix.
 
-usage: python tests/golden/make_stream_golden.py --config 4k --frames 1440
+usage: python tests/golden/make_stream_golden.py --config 4k --frames 1440 [--content noise]
 """
 import argparse
 import json
@@ -35,9 +36,10 @@ CONFIGS = {
 }
 
 
-def path_for(config: str, q: int | None = None) -> str:
+def path_for(config: str, q: int | None = None, content: str = "band4") -> str:
     w, h, ring, q0 = CONFIGS[config]
-    return os.path.join(HERE, f"stream_{config}_q{q if q is not None else q0}_r{ring}.json")
+    sfx = "" if content == "band4" else f"_{content}"
+    return os.path.join(HERE, f"stream_{config}_q{q if q is not None else q0}_r{ring}{sfx}.json")
 
 
 def main():
@@ -46,11 +48,13 @@ def main():
     p.add_argument("--frames", type=int, default=1440)
     p.add_argument("--quality", type=int, default=None)
     p.add_argument("--flush", type=int, default=16)
+    p.add_argument("--content", default="band4", choices=["band4", "noise", "static"])
     a = p.parse_args()
     w, h, ring, q = CONFIGS[a.config]
     if a.quality is not None:
         q = a.quality
-    out = path_for(a.config, q)
+    out = path_for(a.config, q, a.content)
+    from bench import content_frame
     e = orc.OracleEncoder(ring)
     e.set_quality(q)
     bits, fnv = [], []
@@ -59,7 +63,7 @@ def main():
     def dump(final):
         doc = {"_source": "oracle/evx_oracle.c via tests/golden/make_stream_golden.py",
                "config": a.config, "width": w, "height": h, "ring": ring, "quality": q,
-               "content": "band4", "seed": 1234, "first_intra": True,
+               "content": a.content, "seed": 1234 if a.content != "noise" else 7, "first_intra": True,
                "hash": "fnv1a64 of oracle.canonical_frame_bytes(record, bits, t == 0), per frame",
                "frames": len(bits), "complete": final, "frame_bits": bits, "frame_fnv1a64": fnv}
         tmp = out + ".tmp"
@@ -68,7 +72,7 @@ def main():
         os.replace(tmp, out)
 
     for t in range(a.frames):
-        data, n = e.encode(orc.make_frame(w, h, t))
+        data, n = e.encode(content_frame(a.content, w, h, t))
         bits.append(int(n))
         fnv.append(f"{orc.fnv1a64(orc.canonical_frame_bytes(data, n, t == 0)):016x}")
         if (t + 1) % a.flush == 0:

@@ -57,8 +57,9 @@ def main():
     us = lambda ticks: ticks / 100.0  # noqa: E731  (10 ns ticks)
     mbs = max(c["coder_mbs"], 1)
     groups = max(c["helper_tasks"] * ((w + 63) // 64), 1)
-    coder = {k: round(us(c["coder_" + k]) / mbs, 3) for k in ("total", "group_wait", "window", "search", "inter")}
-    coder["rest"] = round(coder["total"] - sum(coder[k] for k in ("group_wait", "window", "search", "inter")), 3)
+    parts = ("group_wait", "window", "search", "inter", "xform", "publish", "drain")
+    coder = {k: round(us(c["coder_" + k]) / mbs, 3) for k in ("total",) + parts}
+    coder["rest"] = round(coder["total"] - sum(coder[k] for k in parts), 3)
     coder["dequeue_per_task"] = round(us(c["coder_dequeue"]) / max(c["coder_tasks"], 1), 2)
     helper = {k: round(us(c["helper_" + k]) / groups, 3) for k in ("total", "wait", "deblock", "search", "catchup")}
     helper["rest"] = round(helper["total"] - sum(helper[k] for k in ("wait", "deblock", "search", "catchup")), 3)

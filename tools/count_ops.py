@@ -25,7 +25,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--configs", default="720p,1080p,4k")
+    ap.add_argument("--content", default="band4", choices=["band4", "noise", "static"],
+                    help="bench.py --content (keys other than band4 get a _<content> suffix)")
     a = ap.parse_args()
+    from bench import content_frame
     out_path = os.path.join(ROOT, "profiles", "algorithmic_ops.json")
     res = json.load(open(out_path)) if os.path.exists(out_path) else {}
     for name in a.configs.split(","):
@@ -35,15 +38,16 @@ def main():
         per = []
         for t in range(a.frames):
             orc.op_counts(reset=True)
-            e.encode(orc.make_frame(w, h, t))
+            e.encode(content_frame(a.content, w, h, t))
             per.append(orc.op_counts())
         p = [c["pixel_ops"] for c in per[1:]]
         mbs = ((w + 15) // 16) * ((h + 15) // 16)
-        res[name] = {"width": w, "height": h, "ring": ring, "quality": q, "baseline_config": idx,
+        key = name if a.content == "band4" else f"{name}_{a.content}"
+        res[key] = {"content": a.content, "width": w, "height": h, "ring": ring, "quality": q, "baseline_config": idx,
                      "frames": a.frames, "per_frame": per,
                      "pixel_ops_per_p_frame": int(sum(p) / len(p)),
                      "pixel_ops_per_mb": round(sum(p) / len(p) / mbs, 1)}
-        print(name, res[name]["pixel_ops_per_p_frame"], res[name]["pixel_ops_per_mb"], flush=True)
+        print(key, res[key]["pixel_ops_per_p_frame"], res[key]["pixel_ops_per_mb"], flush=True)
     json.dump(res, open(out_path, "w"), indent=1)
 
 

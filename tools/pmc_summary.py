@@ -92,6 +92,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r01")
     ap.add_argument("--config", default="720p")
+    ap.add_argument("--content", default="band4", help="bench.py --content of the profiled run")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--steps", type=int, default=20, help="timed launches of the profiled bench.py run")
     ap.add_argument("--batch", type=int, default=0,
@@ -106,9 +107,10 @@ def main():
         a.batch = cairo_amd.default_batch(w, h)
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
+    sfx = "" if a.content == "band4" else f"_{a.content}"
     stats = os.path.join(a.src, "prof_kt", "run_kernel_stats.csv")
     if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(out_dir, f"{a.round}_{a.config}_kernel_stats.csv"))
+        shutil.copy(stats, os.path.join(out_dir, f"{a.round}_{a.config}{sfx}_kernel_stats.csv"))
     fetch = per_kernel(os.path.join(a.src, "prof_fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(a.src, "prof_write", "run_counter_collection.csv"))
     res = {"config": a.config, "round": a.round,
@@ -201,7 +203,7 @@ def main():
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws
-    path = os.path.join(out_dir, f"pmc_{a.config}.json")
+    path = os.path.join(out_dir, f"pmc_{a.config}{sfx}.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res["per_launch_hbm_bytes"]))
 

@@ -3,13 +3,15 @@
 #   rocprofv3 --kernel-trace --stats, then FETCH_SIZE and WRITE_SIZE in their
 #   own --pmc passes (MI355X_MICROARCH.md §HBM).  Only gpurun_out/ comes back
 #   from the box: run tools/pmc_summary.py here afterwards to write profiles/.
-# usage: bash tools/profile_round.sh <round> <config>
+# usage: bash tools/profile_round.sh <round> <config> [content: band4 | noise | static]
 set -e
-R=${1:-r02}; C=${2:-4k}
+R=${1:-r02}; C=${2:-4k}; K=${3:-band4}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/prof_$C
+SFX=$( [ "$K" = band4 ] || echo _$K )
+OUT=gpurun_out/prof_$C$SFX
 rm -rf $OUT && mkdir -p $OUT
-ARGS="--config $C --no-end-to-end --no-cpu-baseline --no-api --no-host-rgb"  # bench.py's default steps / warm-up
+# bench.py's default steps / warm-up; no per-frame check (it adds host work, not GPU work)
+ARGS="--config $C --content $K --no-verify --no-end-to-end --no-cpu-baseline --no-api --no-host-rgb"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_kt -o run -- python3 bench.py $ARGS > $OUT/prof_kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py $ARGS > $OUT/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1
@@ -22,4 +24,4 @@ timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_E
 # L2 (TCC) hits and misses of the reads and writes the CUs send it: the hit
 # rate says how much of the requested window / poll traffic the XCD L2s absorb
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_READ_sum TCC_WRITE_sum --output-format csv -d $OUT/prof_hit -o run -- python3 bench.py $ARGS > $OUT/prof_hit.log 2>&1
-echo "profiled $R $C: now run python tools/pmc_summary.py --round $R --config $C --src gpurun_out/prof_$C locally"
+echo "profiled $R $C $K: now run python tools/pmc_summary.py --round $R --config $C --content $K --src $OUT locally"
