@@ -127,6 +127,10 @@ struct Acct {
   // excluded), publish (granule stores, window update, table), drain (the
   // coefficient drain, the barrier, the info granule)
   static constexpr int kCoderXform = 24, kCoderPublish = 25, kCoderDrain = 26;
+  // before the search: the vmcnt(0) after the window (wave 0), the inter
+  // records and predictions issued inside a group, the barrier
+  static constexpr int kCoderVm0 = 27, kCoderRecords = 28, kCoderPreBarrier = 29;
+  static constexpr int kCoderStoreTail = 30;  // CAIRO_ACCT_STORE_TAIL diagnostic builds
 };
 
 // Frames per engine launch.
@@ -261,6 +265,7 @@ struct EngineArgs {
   size_t plane_elems;
   BlockDesc* table_base;   // stride mbs
   BlockDesc* idesc_base;   // stride nref * mbs
+  void* reserved0;         // (unused: keeps the kernel-argument offsets, see FrameArgs::reserved0)
   uint64_t* gran_base;     // stride mbs * kGranuleStride
   int32_t* sync;           // SyncLayout words of this launch
   int32_t* sticky;         // TimeoutInfo words

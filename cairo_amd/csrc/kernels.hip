@@ -320,6 +320,15 @@ __device__ __forceinline__ uint32_t gran_settle(FA& a, const uint64_t* p, uint64
   return (uint32_t)g;
 }
 
+// p, opaque to the optimiser: the frame view's fields are re-read (scalar
+// loads that hit the scalar cache) in every macroblock instead of being
+// hoisted out of the row loop and kept live in SGPRs, which spill.
+__device__ __forceinline__ FA* opaque_view(FA* p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+s"(v));
+  return (FA*)v;
+}
+
 // Dequeue the next task index for this workgroup (uniform result).
 __device__ __forceinline__ int dequeue(int32_t* ticket, int* lds_slot) {
   __syncthreads();
@@ -984,8 +993,9 @@ __device__ __forceinline__ int inter_need_cols(FA& a, int g, int level) {
 
 // Reference offset `off` of group g of row r: the tagged records of the
 // group's macroblocks are stored and left in flight (the coder polls them).
-__device__ __forceinline__ void inter_task(FA& a, int r, int g, int off, InterLds& L, DbLds& D, DbState& st,
+__device__ __forceinline__ void inter_task(FA& a0, int r, int g, int off, InterLds& L, DbLds& D, DbState& st,
                                            int* flag, uint64_t* is) {
+  FA& a = *opaque_view(&a0);
   const int wave = uni(threadIdx.x >> 6);  // scalar: the acceptance replay runs on SGPRs
   const int x = 4 * g + wave;
   const bool valid = x < a.wmb;
@@ -1440,7 +1450,8 @@ __device__ __forceinline__ bool deblock_chunk_ready(FA& a, int r, const DbState&
 
 // Deblock chunk st.k of MB row r (whole workgroup; waits for its inputs, or
 // known_ready: deblock_chunk_ready said so).
-__device__ __forceinline__ void deblock_chunk(FA& a, int r, DbLds& D, DbState& st, bool known_ready) {
+__device__ __forceinline__ void deblock_chunk(FA& a0, int r, DbLds& D, DbState& st, bool known_ready) {
+  FA& a = *opaque_view(&a0);
   const int tid = threadIdx.x;
   const uint64_t tb = a.stamps && tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint64_t ta = acct_now();
@@ -1877,22 +1888,20 @@ __device__ __forceinline__ const int16_t* plane_of(const PlaneSet& p, int pl) {
   return pick(p, pl);
 }
 
-// Prediction sample of element e (block-major) of the block at (mx, my) of
-// plane set p, lerped toward (mx+dx, my+dy) when sp (macroblock.h:203-259).
-__device__ __forceinline__ int pred_global(const PlaneSet& p, int wa, int e, int mx, int my, bool sp,
-                                           int dx, int dy, int amount) {
+// Sample of element e (block-major) of the block at (mx, my) of plane set p.
+__device__ __forceinline__ int pred_at(const PlaneSet& p, int wa, int e, int mx, int my) {
   if (CAIRO_ATTR_SKIP & 4) return 128;
   int pl, ex, ey;
   elem_coords(e, mx, my, pl, ex, ey);
   const int pitch = pl == 0 ? wa : (wa >> 1);
-  const int16_t* t = plane_of(p, pl);
-  int v = t[(size_t)ey * pitch + ex];
-  if (sp) {
-    int nx, ny;
-    elem_coords(e, mx + dx, my + dy, pl, nx, ny);
-    v = lerp_px(v, t[(size_t)ny * pitch + nx], amount);
-  }
-  return v;
+  return plane_of(p, pl)[(size_t)ey * pitch + ex];
+}
+// Prediction sample of element e (block-major) of the block at (mx, my) of
+// plane set p, lerped toward (mx+dx, my+dy) when sp (macroblock.h:203-259).
+__device__ __forceinline__ int pred_global(const PlaneSet& p, int wa, int e, int mx, int my, bool sp,
+                                           int dx, int dy, int amount) {
+  const int v = pred_at(p, wa, e, mx, my);
+  return sp ? lerp_px(v, pred_at(p, wa, e, mx + dx, my + dy), amount) : v;
 }
 
 // A block descriptor from its four words (all lanes hold the same), fields in
@@ -1953,7 +1962,8 @@ __device__ __forceinline__ void coef_store_pair(FA& a, int e, int px, int py, in
 // kDecode: the decoder's reconstruction (decode_slice, decode.cpp:146-170) from
 // the given block table and coefficients, without the searches.
 template <bool kDecode>
-__device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, int32_t* tr) {
+__device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, int32_t* tr) {
+  FA& a = a0;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int grp = tid >> 4, gi = tid & 15;
   const int thr = (a.quality >> 2) + 1;
@@ -1969,7 +1979,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-    for (int bx = 0; bx < a.wmb; bx++) {
+    for (int bx = 0; bx < a0.wmb; bx++) {
+      FA* ap = opaque_view(&a0);
+#define a (*ap)
       const int px = bx * kMB, mb = by * a.wmb + bx;
       trace(tr, 1, bx);
       trace(tr, 2, (int)a.epoch * 1000 + by);
@@ -1993,6 +2005,13 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // already in, completes behind it (it issues no vector-memory access).
       const bool gstart = (bx & 3) == 0;
       const bool early = !kDecode && gstart;  // workgroup-uniform
+#ifdef CAIRO_ACCT_STORE_TAIL
+      {  // diagnostic (tools builds): how long the previous macroblock's stores still take here
+        const uint64_t ts = acct_now();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        acct_add(a.acct, Acct::kCoderStoreTail, acct_now() - ts);
+      }
+#endif
       uint64_t tacc = acct_now();
       // thread 0: one poll of the group's record count, issued with the fresh
       // granule load and tested after the window update (which waits for it anyway)
@@ -2044,7 +2063,9 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
       // the source DMA has landed (free where the granule wait above covered
       // it): a wait the compiler sees, so it knows no LDS-DMA is in flight and
       // the barrier before the search does not drain the loads issued below
+      const uint64_t tv0 = acct_now();
       if (!kDecode) __builtin_amdgcn_s_waitcnt(kWaitVm0);
+      acct_add(a.acct, Acct::kCoderVm0, acct_now() - tv0);
       if (early && tid == 0) {
         ready0 = by_tag ? (uint32_t)(rd0 >> 32) == a.epoch : (int)rd0 >= a.nref;
         if (ready0) acquire_fence(a.sys);  // completes during the search; waited for after it
@@ -2094,24 +2115,30 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
           inter_d[o] = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
           inter_sad[o] = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
         }
+        // the integer-position block of every reference: its loads overlap
+        // the search (nothing here waits for them); a sub-pel winner's second
+        // block is loaded and lerped after the classification (one
+        // reference, instead of a round trip here for every sub-pel record)
 #pragma unroll
         for (int o = 0; o < kMaxRing - 1; o++) {
           if (o >= nref) break;
           const BlockDesc& d = inter_d[o];
           const PlaneSet rp = RECON_AT(a, d.prediction_target);
-          const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
-          int dx = 0, dy = 0;
-          if (sp) frac_dir(d.sp_index, &dx, &dy);
+          const bool mot = (d.block_type & kMotion) != 0;
           _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
-            ipv[o][bi] = pred_global(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
-                                     py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
+            ipv[o][bi] = pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
+                                 py + (mot ? d.motion_y : 0));
         }
       };
+      const uint64_t tr0 = acct_now();
       if (!early) load_inter();
       stamp(a, mb, 1);
+      const uint64_t tr1 = acct_now();
       __syncthreads();
       stamp(a, mb, 2);
       tacc = acct_now();
+      acct_add(a.acct, Acct::kCoderRecords, tr1 - tr0);
+      acct_add(a.acct, Acct::kCoderPreBarrier, tacc - tr1);
 
       BlockDesc d;
       bool from_inter = false;  // an inter record won / an inter type is decoded (prediction in wpv)
@@ -2211,6 +2238,14 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
             wpv[1] = ipv[o][1];
           }
         }
+        if (from_inter && (d.block_type & kMotion) && d.sp_pred) {  // the winner's sub-pel lerp
+          const PlaneSet rp = RECON_AT(a, d.prediction_target);
+          int dx, dy;
+          frac_dir(d.sp_index, &dx, &dy);
+          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
+            wpv[bi] = lerp_px(wpv[bi], pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + d.motion_x + dx,
+                                               py + d.motion_y + dy), d.sp_amount);
+        }
       } else {
         // ---- decoder (decode_slice, decode.cpp:146-170): the block desc is
         //      given; an inter type predicts from its reference slot ----
@@ -2228,6 +2263,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
                                   py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
         }
       }
+      ap = opaque_view(ap);  // after the searches: the view's fields re-read, not live across them
       stamp(a, mb, 5);
       const uint64_t tx5 = acct_now();
       // this lane's source elements for the residual, loaded after the
@@ -2389,6 +2425,7 @@ __device__ __forceinline__ void code_row(FA& a, int by, RowLds& L, int* flag, in
         acct_add(a.acct, Acct::kCoderDrain, tx9 - tx8);
       }
       if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
+#undef a
     }
   }
 }
@@ -2414,12 +2451,14 @@ struct EngineLds {
 // coder waits for exactly these), and the deblock of row r, chunk by chunk as
 // the coder's granules arrive (advanced whenever the inter search is waiting
 // or done).  Never blocks on its own row coder while an inter group is due.
-__device__ __forceinline__ void row_helper(FA& a, int r, HelperLds& L, int* flag, int32_t* tr) {
+__device__ __forceinline__ void row_helper(FA& a0, int r, HelperLds& L, int* flag, int32_t* tr) {
+  FA& a = a0;
   const int tid = threadIdx.x;
   const int nch = db_chunks(a);
   volatile int* vflag = flag;
   DbState st{0, 0, 0, 8};
-  for (int g = 0; g < a.ng; g++) {
+  for (int g = 0; g < a0.ng; g++) {
+    FA& a = *opaque_view(&a0);
     trace(tr, 1, g);
     trace(tr, 2, (int)a.epoch * 1000 + r);
     uint64_t* is = a.istamps && tid == 0 ? a.istamps + (size_t)(r * a.ng + g) * kIStamps : nullptr;

@@ -57,7 +57,8 @@ def main():
     us = lambda ticks: ticks / 100.0  # noqa: E731  (10 ns ticks)
     mbs = max(c["coder_mbs"], 1)
     groups = max(c["helper_tasks"] * ((w + 63) // 64), 1)
-    parts = ("group_wait", "window", "search", "inter", "xform", "publish", "drain")
+    parts = ("group_wait", "window", "search", "inter", "xform", "publish", "drain", "vm0", "records", "prebarrier",
+             "store_tail")
     coder = {k: round(us(c["coder_" + k]) / mbs, 3) for k in ("total",) + parts}
     coder["rest"] = round(coder["total"] - sum(coder[k] for k in parts), 3)
     coder["dequeue_per_task"] = round(us(c["coder_dequeue"]) / max(c["coder_tasks"], 1), 2)
