@@ -2005,6 +2005,23 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       // already in, completes behind it (it issues no vector-memory access).
       const bool gstart = (bx & 3) == 0;
       const bool early = !kDecode && gstart;  // workgroup-uniform
+      // The macroblock's inter records (2 * nref tagged granules; every lane
+      // of a wave the same addresses): inside a group they are normally in
+      // already, so their loads go out here, in flight with the fresh
+      // granule's, instead of a round trip of their own after it (settled by
+      // tag in load_inter).  At a group start, after the search.
+      const int nref = a.inter ? a.ring - 1 : 0;
+      uint64_t rg[kMaxRing - 1][2];
+      auto issue_records = [&]() {
+#pragma unroll
+        for (int o = 0; o < kMaxRing - 1; o++) {
+          if (o >= nref) break;
+          const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
+          rg[o][0] = gran_ld(r);
+          rg[o][1] = gran_ld(r + 1);
+        }
+      };
+      if (!early) issue_records();
 #ifdef CAIRO_ACCT_STORE_TAIL
       {  // diagnostic (tools builds): how long the previous macroblock's stores still take here
         const uint64_t ts = acct_now();
@@ -2093,41 +2110,35 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       }
 
       // ---- inter predictions, prefetched (the K1 records are final) ----
-      BlockDesc inter_d[kMaxRing - 1];
-      int inter_sad[kMaxRing - 1];
-      int ipv[kMaxRing - 1][2];
-      const int nref = a.inter ? a.ring - 1 : 0;
-      auto load_inter = [&]() {
-        // each wave loads the macroblock's 2 * nref record granules (every
-        // lane the same addresses), all issued before the first is tested
-        uint64_t rg[kMaxRing - 1][2];
+      // the prediction of the best inter record: the classification below
+      // is a lexicographic minimum of (not copy, sad) over [intra, ref 1..],
+      // the earlier winning ties, so the only inter record that can win is
+      // the minimum over the references alone -- known from the records,
+      // before the search.  Its block (and a sub-pel winner's neighbour)
+      // loads overlap the search.
+      BlockDesc ib;
+      int ib_sad = 0;
+      int ipa[2] = {0, 0}, ipb[2] = {0, 0};
+      auto load_inter = [&]() {  // the records (issue_records), then the predictions
 #pragma unroll
         for (int o = 0; o < kMaxRing - 1; o++) {
           if (o >= nref) break;
           const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
-          rg[o][0] = gran_ld(r);
-          rg[o][1] = gran_ld(r + 1);
+          const BlockDesc rd = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
+          const int rs = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
+          const bool ci = (rd.block_type & kCopy) != 0, cb = (ib.block_type & kCopy) != 0;
+          if (o == 0 || (ci != cb ? ci : rs < ib_sad)) ib = rd, ib_sad = rs;
         }
-#pragma unroll
-        for (int o = 0; o < kMaxRing - 1; o++) {
-          if (o >= nref) break;
-          const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
-          inter_d[o] = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
-          inter_sad[o] = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
-        }
-        // the integer-position block of every reference: its loads overlap
-        // the search (nothing here waits for them); a sub-pel winner's second
-        // block is loaded and lerped after the classification (one
-        // reference, instead of a round trip here for every sub-pel record)
-#pragma unroll
-        for (int o = 0; o < kMaxRing - 1; o++) {
-          if (o >= nref) break;
-          const BlockDesc& d = inter_d[o];
-          const PlaneSet rp = RECON_AT(a, d.prediction_target);
-          const bool mot = (d.block_type & kMotion) != 0;
-          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
-            ipv[o][bi] = pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
-                                 py + (mot ? d.motion_y : 0));
+        if (nref == 0) return;
+        const BlockDesc& d = ib;
+        const PlaneSet rp = RECON_AT(a, d.prediction_target);
+        const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
+        const int mx = px + (mot ? d.motion_x : 0), my = py + (mot ? d.motion_y : 0);
+        int dx = 0, dy = 0;
+        if (sp) frac_dir(d.sp_index, &dx, &dy);
+        _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
+          ipa[bi] = pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, mx, my);
+          if (sp) ipb[bi] = pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, mx + dx, my + dy);
         }
       };
       const uint64_t tr0 = acct_now();
@@ -2219,6 +2230,7 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
           tacc = acct_now();
           if (tid < kGranulesPerMB && pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);
+          issue_records();
           load_inter();
           acct_add(a.acct, Acct::kCoderInter, acct_now() - tacc);
         }
@@ -2226,25 +2238,20 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         int best_sad = sel.sad;
 
         // ---- classify_block (encode.cpp:17-67) ----
-  #pragma unroll
-        for (int o = 0; o < kMaxRing - 1; o++) {
-          if (o >= nref) break;
-          const bool ci = (inter_d[o].block_type & kCopy) != 0, cb = (d.block_type & kCopy) != 0;
-          if (ci != cb ? ci : inter_sad[o] < best_sad) {
-            d = inter_d[o];
-            best_sad = inter_sad[o];
+        if (nref > 0) {
+          const bool ci = (ib.block_type & kCopy) != 0, cb = (d.block_type & kCopy) != 0;
+          if (ci != cb ? ci : ib_sad < best_sad) {
+            d = ib;
+            best_sad = ib_sad;
             from_inter = true;
-            wpv[0] = ipv[o][0];
-            wpv[1] = ipv[o][1];
+            const bool sp = (d.block_type & kMotion) && d.sp_pred;
+            _Pragma("unroll") for (int bi = 0; bi < 2; bi++) {
+              // pinned here: the lerp would otherwise be hoisted above the
+              // search, waiting for the loads there
+              asm volatile("" : "+v"(ipa[bi]), "+v"(ipb[bi]));
+              wpv[bi] = sp ? lerp_px(ipa[bi], ipb[bi], d.sp_amount) : ipa[bi];
+            }
           }
-        }
-        if (from_inter && (d.block_type & kMotion) && d.sp_pred) {  // the winner's sub-pel lerp
-          const PlaneSet rp = RECON_AT(a, d.prediction_target);
-          int dx, dy;
-          frac_dir(d.sp_index, &dx, &dy);
-          _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
-            wpv[bi] = lerp_px(wpv[bi], pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + d.motion_x + dx,
-                                               py + d.motion_y + dy), d.sp_amount);
         }
       } else {
         // ---- decoder (decode_slice, decode.cpp:146-170): the block desc is
