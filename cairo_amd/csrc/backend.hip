@@ -536,8 +536,7 @@ int flush(cairo_ctx* c) {
   // launch takes at most half of the engine's resident
   // workgroup slots (CUs x occupancy, measured at create: 256 x 3 = 768 on a
   // full MI355X), so two launches are always co-resident.  Every row has a
-  // coder and a helper (inter search + deblock) living as long as the row:
-  // equal pools.  The pools are shared: launch b's workers take b-1's
+  // coder task and a helper (inter search + deblock) task: two pools.  The pools are shared: launch b's workers take b-1's
   // remaining tasks first (all of them are older), so b-1's tail is not left
   // to b-1's own workers; a batch is complete when its finished-task count
   // says so (k_batch_wait), not when its launch ends.
@@ -553,7 +552,9 @@ int flush(cairo_ctx* c) {
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
   {  // half of the resident slots per launch, split between the pools
     const int total = 2 * (c->wg_rows > 0 ? std::min(c->wg_rows, (c->stamps ? 2 : 1) * c->max_rows) : c->max_rows);
-    int nh = c->wg_helpers > 0 ? std::min(c->wg_helpers, total - 1) : total / 2;
+    // default split: 25/48 helpers (200 of 384), measured best at 4K
+    // (profiles/r05/sweep_helpers.txt); multiples of kLabels keep both pools banded
+    int nh = c->wg_helpers > 0 ? std::min(c->wg_helpers, total - 1) : std::max(1, (total * 25 / 48) & ~(kLabels - 1));
     int nr = total - nh;
     e.n_helpers = std::max(1, std::min(nh, rows));
     e.n_rows = std::max(1, std::min(nr, rows));
@@ -848,8 +849,8 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
     }                                  \
   } while (0)
   TRY(hipSetDevice(device));
-  {  // engine pools per launch: half of the resident workgroup slots, halved
-     // again between helpers and row coders
+  {  // engine pools per launch: half of the resident workgroup slots, split
+     // between helpers and row coders at submit
     int cus = 0, per_cu = 0;
     TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     TRY(engine_blocks_per_cu(&per_cu));
