@@ -74,7 +74,10 @@ __constant__ int16_t kBeta[32] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 3
 // LDS copies of the tables, loaded once per workgroup (load_tables): a lookup
 // with a per-lane index is then an LDS read (lgkmcnt) instead of a global load
 // whose vmcnt(0) wait would also drain the outstanding hand-off loads.
-__shared__ int16_t sLut8[64], sQmIntra[64], sQmInter[64], sAlpha[32], sBeta[32];
+// sLut8T (the transpose) makes every transform pass's 8 coefficients one
+// 16-byte row read.
+__shared__ __attribute__((aligned(16))) int16_t sLut8[64], sLut8T[64];
+__shared__ int16_t sQmIntra[64], sQmInter[64], sAlpha[32], sBeta[32];
 // Reciprocals for the quantizer's divisions (rdiv_m): the matrices' entries,
 // 2 qp and the DC scales for qp = 0..31.
 __shared__ uint32_t sMagQmIntra[64], sMagQmInter[64], sMag2qp[32], sMagDcL[32], sMagDcC[32];
@@ -96,6 +99,7 @@ __device__ __forceinline__ void load_tables() {
   const int t = threadIdx.x;
   if (t < 64) {
     sLut8[t] = kLut8[t];
+    sLut8T[t] = kLut8[(t & 7) * 8 + (t >> 3)];
     sQmIntra[t] = kQmIntra[t];
     sQmInter[t] = kQmInter[t];
   } else if (t < 96) {
@@ -1236,18 +1240,18 @@ __device__ __forceinline__ int fdct_lane(int16_t* sa, int16_t* sb, int lane, int
   sa[lane] = x;
   __builtin_amdgcn_wave_barrier();
   {
-    const int8v row = load_row8(&sa[r8 * 8]);
+    const int8v row = load_row8(&sa[r8 * 8]), lut = load_row8(&sLut8[c8 * 8]);
     int t = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) t += row[k] * sLut8[c8 * 8 + k];
+    for (int k = 0; k < 8; k++) t += row[k] * lut[k];
     t = c8 == 0 ? (t * 45) / 128 : t / 2;
     sb[c8 * 8 + r8] = (int16_t)rdiv(t, 128);  // transposed
   }
   __builtin_amdgcn_wave_barrier();
-  const int8v col = load_row8(&sb[c8 * 8]);  // column c8 of the row pass
+  const int8v col = load_row8(&sb[c8 * 8]), lut = load_row8(&sLut8[r8 * 8]);  // column c8 of the row pass
   int t = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) t += col[k] * sLut8[r8 * 8 + k];
+  for (int k = 0; k < 8; k++) t += col[k] * lut[k];
   t = r8 == 0 ? (t * 45) / 128 : t / 2;
   return (int16_t)rdiv(t, 128);
 }
@@ -1260,17 +1264,17 @@ __device__ __forceinline__ int idct_lane(int16_t* sa, int16_t* sb, int lane, int
   sa[c8 * 8 + r8] = d;  // transposed: row c8 of sa = column c8
   __builtin_amdgcn_wave_barrier();
   {
-    const int8v col = load_row8(&sa[c8 * 8]);
-    int t = ((col[0] * sLut8[r8]) * 45) / 128;
+    const int8v col = load_row8(&sa[c8 * 8]), lut = load_row8(&sLut8T[r8 * 8]);  // lut[k] = sLut8[k * 8 + r8]
+    int t = ((col[0] * lut[0]) * 45) / 128;
 #pragma unroll
-    for (int k = 1; k < 8; k++) t += (col[k] * sLut8[k * 8 + r8]) / 2;
+    for (int k = 1; k < 8; k++) t += (col[k] * lut[k]) / 2;
     sb[r8 * 8 + c8] = (int16_t)rdiv(t, 128);
   }
   __builtin_amdgcn_wave_barrier();
-  const int8v row = load_row8(&sb[r8 * 8]);
-  int t = ((row[0] * sLut8[c8]) * 45) / 128;
+  const int8v row = load_row8(&sb[r8 * 8]), lut = load_row8(&sLut8T[c8 * 8]);
+  int t = ((row[0] * lut[0]) * 45) / 128;
 #pragma unroll
-  for (int k = 1; k < 8; k++) t += (row[k] * sLut8[k * 8 + c8]) / 2;
+  for (int k = 1; k < 8; k++) t += (row[k] * lut[k]) / 2;
   return rdiv(t, 128);
 }
 
