@@ -17,6 +17,9 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fe
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1
 # wave states of the engine (8 SQ counters + GRBM_GUI_ACTIVE, one pass)
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/prof_sq -o run -- python3 bench.py $ARGS > $OUT/prof_sq.log 2>&1
+# LDS: instructions, bank-conflict and unaligned-stall cycles against all
+# LDS-array cycles, and the waves' LDS issue stalls
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/prof_lds -o run -- python3 bench.py $ARGS > $OUT/prof_lds.log 2>&1
 # read requests by size, and the uncached 32-byte ones (the hand-off polls and
 # granule loads), so the traffic needs no blanket FETCH_SIZE correction
 timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RD_UNCACHED_32B_sum --output-format csv -d $OUT/prof_rdsize -o run -- python3 bench.py $ARGS > $OUT/prof_rdsize.log 2>&1
