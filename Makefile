@@ -55,6 +55,7 @@ check-knobs:
 	$(HIPCC) $(HIPFLAGS) -DCAIRO_ACCT=1 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/acct.o
 	$(HIPCC) $(HIPFLAGS) -DCAIRO_TOOLS_BUILD -DCAIRO_ATTR_SKIP=1 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/attr1.o
 	$(HIPCC) $(HIPFLAGS) -DCAIRO_TOOLS_BUILD -DCAIRO_ATTR_SKIP=4 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/attr4.o
+	$(HIPCC) $(HIPFLAGS) -DCAIRO_TOOLS_BUILD -DCAIRO_ATTR_SKIP=120 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/attr120.o
 	$(HIPCC) $(HIPFLAGS) -DCAIRO_MAX_BATCH=64 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/batch64.o
 	$(HIPCC) $(HIPFLAGS) -DCAIRO_MAX_BATCH=64 -c $(SRC)/backend.hip -o $(KNOB_OBJ)/batch64_backend.o
 	@if $(HIPCC) $(HIPFLAGS) -DCAIRO_ATTR_SKIP=1 -c $(SRC)/kernels.hip -o $(KNOB_OBJ)/refused.o 2>/dev/null; then \

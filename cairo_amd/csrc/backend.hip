@@ -552,9 +552,11 @@ int flush(cairo_ctx* c) {
   for (int i = 0; i < c->npend; i++) fh[i] = make_frame_view(e, c->pend[i], i);
   {  // half of the resident slots per launch, split between the pools
     const int total = 2 * (c->wg_rows > 0 ? std::min(c->wg_rows, (c->stamps ? 2 : 1) * c->max_rows) : c->max_rows);
-    // default split: 25/48 helpers (200 of 384), measured best at 4K
-    // (profiles/r05/sweep_helpers.txt); multiples of kLabels keep both pools banded
-    int nh = c->wg_helpers > 0 ? std::min(c->wg_helpers, total - 1) : std::max(1, (total * 25 / 48) & ~(kLabels - 1));
+    // default split: even, and 25/48 helpers (200 of 384) on large frames
+    // (kernels.h kPrioFrameMBs); multiples of kLabels keep both pools banded
+    const bool large = (int)c->wmb * (int)c->hmb > kPrioFrameMBs;
+    int nh = c->wg_helpers > 0 ? std::min(c->wg_helpers, total - 1)
+                               : (large ? std::max(1, (total * 25 / 48) & ~(kLabels - 1)) : total / 2);
     int nr = total - nh;
     e.n_helpers = std::max(1, std::min(nh, rows));
     e.n_rows = std::max(1, std::min(nr, rows));

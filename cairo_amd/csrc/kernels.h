@@ -300,7 +300,13 @@ struct EngineArgs {
 // at most on frame f-1, row r+3, so any slope > 3 keeps every wait pointing
 // to an earlier key (deadlock-free), while frames interleave in the pools
 // instead of queueing behind each other.
-constexpr int kOrderSlope = 5;  // (4 and 6 measured slower)
+constexpr int kOrderSlope = 5;  // (4 and 6 slower in rounds 2-3; within 0.3 % in round 5, profiles/r05/ab_4k_order_slope.txt)
+
+// Large frames (more macroblocks than this): the helpers get SIMD issue
+// priority (kernels.hip k_engine) and a larger share of a launch's workers
+// (backend.hip, 200 of 384: measured best at 4K and 1080p, 0.6 % behind the
+// even split at 720p, profiles/r05/sweep_helpers.txt).
+constexpr int kPrioFrameMBs = 4000;
 
 // XCD-banded queues: on a frame of at least kBandMinRows macroblock rows each
 // pool keeps one queue per label (kLabels), and a worker serves the queue of

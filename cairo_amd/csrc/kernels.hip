@@ -454,7 +454,8 @@ __device__ __forceinline__ uint4 bias4(uint4 v) {
 // shapes, wrong results -- so the drop in fabric reads against the default
 // build is what those loads cost.  Instructions: bit 8 skips the helpers'
 // integer and sub-pel steps (zero-MV records), bit 16 the row coders' intra
-// search (stages and sub-pel), bit 32 the deblock filters; the drop in
+// search (stages and sub-pel), bit 32 the deblock filters, bit 64 the row
+// coders' transform chain (DCT, quantize, dequantize, IDCT); the drop in
 // SQ_INSTS_VALU is what those phases issue (the decisions change too, so the
 // other phases' counts move a little).  Refused unless the build says it is a
 // tools build.
@@ -2322,8 +2323,8 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           int pl, ex, ey;
           elem_coords(e, px, py, pl, ex, ey);
           const int sv = svp[bi];
-          cf[bi] = fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
-                             has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv);
+          const int16_t res = has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv;
+          cf[bi] = (CAIRO_ATTR_SKIP & 64) ? res : fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane, res);
         }
       }
       stamp(a, mb, 6);
@@ -2341,15 +2342,16 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           const int b = wave + 4 * bi, e = b * 64 + lane;
           int16_t qv;
           if (!kDecode) {
-            qv = quant_elem(e, cf[bi], qp, intra_path);
+            qv = (CAIRO_ATTR_SKIP & 64) ? (int16_t)cf[bi] : quant_elem(e, cf[bi], qp, intra_path);
             coef_store_pair(a, e, px, py, qv);
           } else {  // the decoded coefficients (the decoder's input_cache)
             int pl, ex, ey;
             elem_coords(e, px, py, pl, ex, ey);
             qv = plane_of(planes(a.coef), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
           }
-          const int t = idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
-                                  dequant_elem(e, qv, qp, intra_path));
+          const int t = (CAIRO_ATTR_SKIP & 64) ? qv
+                                               : idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
+                                                           dequant_elem(e, qv, qp, intra_path));
           pv[bi] = (int16_t)(has_pred ? t + pv[bi] : t);  // reconstruction (unclamped)
         }
       } else {  // copy: output_cache keeps this macroblock's previous coefficients
@@ -2550,7 +2552,6 @@ __device__ __forceinline__ void row_helper(FA& a0, int r, HelperLds& L, int* fla
 // deadlock with every workgroup resident.
 // ---------------------------------------------------------------------------
 
-constexpr int kPrioFrameMBs = 4000;  // helpers get issue priority above this frame size
 constexpr int kPrioLevel = 2;        // (1 and 3 measured the same)
 
 // Pool of workgroup b out of n, nh of them helpers: spread evenly over the

@@ -6,6 +6,7 @@ Inputs (gpurun_out/, written by the rocprofv3 commands in DESIGN.md §Measuremen
   prof_write/run_counter_collection.csv --pmc WRITE_SIZE  (own pass)
   prof_sq/run_counter_collection.csv    --pmc SQ_* + GRBM_GUI_ACTIVE (wave states, optional)
   prof_hit/run_counter_collection.csv   --pmc TCC_HIT/MISS/READ/WRITE_sum (L2 hit rate, optional)
+  prof_lds/run_counter_collection.csv   --pmc SQ_LDS_* + SQ_INSTS_LDS (LDS use and conflicts, optional)
 
 Outputs:
   profiles/<round>_<config>_kernel_stats.csv  (copy of the stats summary)
@@ -200,6 +201,24 @@ def main():
                                 "hit_rate": round(hit / max(hit + miss, 1), 4),
                                 "reads_per_frame": int(med.get("TCC_READ_sum", 0) / a.batch),
                                 "writes_per_frame": int(med.get("TCC_WRITE_sum", 0) / a.batch)}
+    # LDS (one pass): indexed-access cycles per CU against the dispatch's
+    # cycles, and the share of them spent on bank conflicts / unaligned stalls
+    lp = os.path.join(a.src, "prof_lds", "run_counter_collection.csv")
+    if os.path.exists(lp):
+        med = {}
+        for cn in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_UNALIGNED_STALL",
+                   "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
+            v = per_kernel(lp, cn).get("engine")
+            if v:
+                med[cn] = statistics.median(v)
+        if "SQ_LDS_IDX_ACTIVE" in med and "GRBM_GUI_ACTIVE" in med:
+            idx = med["SQ_LDS_IDX_ACTIVE"]
+            res["engine_lds"] = {"median_per_dispatch": med,
+                                 "lds_busy_frac_per_cu": round(idx / 256 / (med["GRBM_GUI_ACTIVE"] / 8.0), 4),
+                                 "bank_conflict_share": round(med.get("SQ_LDS_BANK_CONFLICT", 0) / max(idx, 1), 4),
+                                 "unaligned_stall_share": round(med.get("SQ_LDS_UNALIGNED_STALL", 0) / max(idx, 1), 4),
+                                 "lds_issue_stall_frac_of_wave_time":
+                                     round(med.get("SQ_WAIT_INST_LDS", 0) / max(med.get("SQ_WAVE_CYCLES", 1), 1), 4)}
     ws = wave_states(os.path.join(a.src, "prof_sq", "run_counter_collection.csv"))
     if ws:
         res["engine_wave_states"] = ws
