@@ -174,7 +174,7 @@ struct cairo_ctx {
   size_t feed_words = 0;          // per staging slot
   uint32_t* feed_dev = nullptr;   // [stages][feed_words]
   uint32_t* feed_hdr = nullptr;   // [stages][kFeedHdrWords]
-  uint32_t* feed_scratch = nullptr;  // [stages][kFeedScratchPerMB * mbs]
+  uint32_t* feed_scratch = nullptr;  // [stages][feed_scratch_words(mbs)]
   uint32_t* feed_host = nullptr;  // mapped pinned [stages][kFeedHdrWords + feed_words]
   hipStream_t fs = nullptr;       // synchronous coefficient fetches (a frame whose feed overflowed)
   // The precode runs on a stream of its own after each launch, filling the
@@ -182,6 +182,7 @@ struct cairo_ctx {
   // next launch back (A/B at 4K: 3583 vs 3768 Mpix/s).
   hipStream_t ps = nullptr;
   hipEvent_t pre_done[kSyncAreas] = {};
+  hipEvent_t kernel_end[kSyncAreas] = {};  // (precode on its own stream) the engine kernel of that area's launch ended
   bool ps_own = getenv("CAIRO_PRECODE_OWN_STREAM") != nullptr;  // A/B switch
   bool sys = false;           // a member is another process or device: system-scope hand-offs
   int32_t *sync = nullptr;
@@ -435,6 +436,8 @@ void free_ctx(cairo_ctx* c) {
   if (c->fs) (void)hipStreamDestroy(c->fs);
   for (auto& ev : c->pre_done)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->kernel_end)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->ps) (void)hipStreamDestroy(c->ps);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
   leave_group(c);
@@ -632,8 +635,17 @@ int flush(cairo_ctx* c) {
   if (tb) CK(hipEventRecord(tb->ev[2], st));
   CK(launch_engine(e, st));
   // the launch ends when its workers find no task left; its batch is done
-  // when every task has finished (the next launch's workers may run the last)
-  CK(launch_batch_wait(e.sync, 2 * rows, c->sticky, st));
+  // when every task has finished (the next launch's workers may run the last).
+  // With the precode on a stream of its own the wait for that runs there too,
+  // so that the launch two ahead on this stream starts when this kernel ends,
+  // not after the previous launch's last tasks and the precode.
+  const bool own = c->ps_own && c->ps;
+  hipStream_t bst = own ? c->ps : st;
+  if (own) {
+    CK(hipEventRecord(c->kernel_end[area], st));
+    CK(hipStreamWaitEvent(c->ps, c->kernel_end[area], 0));
+  }
+  CK(launch_batch_wait(e.sync, 2 * rows, c->sticky, bst));
   c->prev_fa = fd;
   for (int k = 0; k < 2; k++) c->prev_order[k] = e.order[k], c->prev_seg[k] = e.seg[k];
   c->prev_sync = e.sync;
@@ -647,11 +659,10 @@ int flush(cairo_ctx* c) {
   }
   const int last = c->pend[e.nframes - 1].slot;
   const uint32_t last_epoch = c->pend[e.nframes - 1].epoch;
-  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
-  hipStream_t pst = c->ps_own ? c->ps : st;
-  if (c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
+  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), bst));
+  hipStream_t pst = bst;
+  if (own) CK(hipEventRecord(c->batch_end[area], bst));
   if (c->outputs & CAIRO_OUT_FEED) {  // the entropy precode, straight into mapped host memory
-    if (c->ps_own) CK(hipStreamWaitEvent(c->ps, c->batch_end[area], 0));
     FeedArgs fa;
     memset(&fa, 0, sizeof(fa));
     fa.nframes = e.nframes;
@@ -661,7 +672,7 @@ int flush(cairo_ctx* c) {
       fa.host[i] = c->feed_host + (size_t)fa.slot[i] * (kFeedHdrWords + c->feed_words);
     }
     fa.scratch = c->feed_scratch;
-    fa.scratch_stride = kFeedScratchPerMB * c->mbs;
+    fa.scratch_stride = feed_scratch_words(c->mbs);
     fa.feed = c->feed_dev;
     fa.feed_stride = c->feed_words;
     fa.hdr = c->feed_hdr;
@@ -676,12 +687,12 @@ int flush(cairo_ctx* c) {
     fa.table_words = (int)(c->mbs * sizeof(BlockDesc) / sizeof(uint4));
     CK(launch_precode(fa, (int)c->mbs, pst));
   }
-  if (!c->ps_own) CK(hipEventRecord(c->batch_end[area], st));
+  if (!own) CK(hipEventRecord(c->batch_end[area], st));
   // the copy stream carries D2H copies only with the coefficient planes; in
   // feed-only mode it carries the host-RGB uploads (submit), which must not
   // queue behind the launches in flight
   if (c->outputs & CAIRO_OUT_COEF) {
-    if (c->ps_own && (c->outputs & CAIRO_OUT_FEED)) {
+    if (own && (c->outputs & CAIRO_OUT_FEED)) {
       CK(hipEventRecord(c->pre_done[area], c->ps));
       CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
     } else {
@@ -1295,7 +1306,7 @@ int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
     uint32_t *dev = nullptr, *hdr = nullptr, *scratch = nullptr, *host = nullptr;
     hipError_t e = hipMalloc(&dev, words * 4 * S);
     if (e == hipSuccess) e = hipMalloc(&hdr, kFeedHdrWords * 4 * S);
-    if (e == hipSuccess) e = hipMalloc(&scratch, kFeedScratchPerMB * c->mbs * 4 * S);
+    if (e == hipSuccess) e = hipMalloc(&scratch, feed_scratch_words(c->mbs) * 4 * S);
     if (e == hipSuccess) e = hipHostMalloc(&host, (kFeedHdrWords + words) * 4 * S, hipHostMallocMapped);
     if (e != hipSuccess) {
       for (void* q : {(void*)dev, (void*)hdr, (void*)scratch}) (void)hipFree(q);
@@ -1307,6 +1318,7 @@ int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
     if (c->ps_own && !c->ps) {  // (the A/B variant: each stream takes a hardware queue)
       CK(hipStreamCreateWithFlags(&c->ps, hipStreamNonBlocking));
       for (auto& ev : c->pre_done) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      for (auto& ev : c->kernel_end) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
   }
   c->outputs = outputs;

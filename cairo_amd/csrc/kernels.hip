@@ -2328,6 +2328,22 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         }
       }
       stamp(a, mb, 6);
+      // The prefetched window blocks for MB bx+1 (loaded before the search),
+      // into the window before this macroblock's first store: settled after
+      // the stores, their wait (vmcnt retires in order) also waited for the
+      // stores' write-through acknowledgements.  This macroblock no longer
+      // reads the cells they land in: block bx+3 is beyond its search's reach
+      // (px+47), and the stale block (bx, by+1) lies where its candidates are
+      // not yet coded.
+      if (tid < kGranulesPerMB) {
+        if (pf3)
+          win_put_k(L.win, oy, bx + 3, by - 3, tid,
+                    gran_settle(a, gran_at(a, bx + 3, by - 3, tid), pg3, by));
+        if (pf2)
+          win_put_k(L.win, oy, bx + 3, by - 2, tid,
+                    gran_settle(a, gran_at(a, bx + 3, by - 2, tid), pg2, by));
+        if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
+      }
       if (!(type & kCopy)) {
         int qp;
         if (!kDecode) {
@@ -2396,15 +2412,6 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         int pl, ex, ey;
         elem_coords(e, px, py, pl, ex, ey);
         win_put1(L.win, pl, pl == 0 ? ey - oy : ey - (oy >> 1), ex, pv[bi]);
-      }
-      if (tid < kGranulesPerMB) {  // prefetched window blocks for MB bx+1
-        if (pf3)
-          win_put_k(L.win, oy, bx + 3, by - 3, tid,
-                    gran_settle(a, gran_at(a, bx + 3, by - 3, tid), pg3, by));
-        if (pf2)
-          win_put_k(L.win, oy, bx + 3, by - 2, tid,
-                    gran_settle(a, gran_at(a, bx + 3, by - 2, tid), pg2, by));
-        if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
       asm volatile("" ::: "memory");  // ... the pixel-granule stores, then the table store
       if (tid == 0 && !kDecode) *(uint4*)&a.table[mb] = __builtin_bit_cast(uint4, d);  // one 16-byte store

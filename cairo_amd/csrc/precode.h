@@ -12,8 +12,13 @@ namespace cairo {
 // each of the 11 lists (8 block-table lists, the Y, U and V sections).
 constexpr int kFeedHdrWords = 16;
 // Per-slot scratch words per macroblock: block lengths [6], table codes [8],
-// table positions [8], section offsets [3].
+// table positions [8], section offsets [3]; then one record per chunk of
+// kFeedChunk macroblocks (the scan's chunk aggregates / carry-ins).
 constexpr int kFeedScratchPerMB = 25;
+constexpr int kFeedChunk = 256, kFeedChunkWords = 20;
+inline size_t feed_scratch_words(size_t mbs) {
+  return kFeedScratchPerMB * mbs + kFeedChunkWords * ((mbs + kFeedChunk - 1) / kFeedChunk);
+}
 
 // Feed capacity per staging slot, in 32-bit words: the table lists (at most
 // 103 bits per macroblock with 31-bit exp-Golomb codes) plus three
@@ -27,7 +32,7 @@ struct FeedArgs {
   const FrameArgs* fa;            // the launch's frame views (device)
   int slot[kMaxBatch];            // staging slot of frame j
   uint32_t* host[kMaxBatch];      // frame j's mapped pinned host buffer: header, then words
-  uint32_t* scratch;              // per slot: kFeedScratchPerMB * mbs words
+  uint32_t* scratch;              // per slot: feed_scratch_words(mbs) words
   size_t scratch_stride;
   uint32_t* feed;                 // per slot: feed words (device)
   size_t feed_stride;
@@ -40,7 +45,8 @@ struct FeedArgs {
   int table_words;
 };
 
-// k_feed_len -> k_feed_scan -> k_feed_write -> k_feed_copy for every frame of a launch.
+// k_feed_len -> k_feed_agg -> k_feed_carry -> k_feed_scan -> k_feed_write ->
+// k_feed_copy for every frame of a launch.
 hipError_t launch_precode(const FeedArgs& f, int mbs, hipStream_t s);
 
 }  // namespace cairo

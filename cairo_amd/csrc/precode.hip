@@ -11,15 +11,16 @@
 //   BR), then U, then V, each block ue(run) + se(zig-zag coefficients) with a
 //   delta DC.
 //
-// Four kernels per launch, on the launch's stream after the engine:
+// Six kernels per launch, on the launch's stream after the engine:
 //   k_feed_len    one wave per macroblock: the bits of its six 8x8 blocks
 //                 (zig-zag in lanes, the run from a ballot, exp-Golomb
 //                 lengths summed)
-//   k_feed_scan   one 256-thread workgroup per frame over chunks of 256
-//                 macroblocks: the table items' codes (segmented "previous
-//                 value" scans for the delta lists) and the exclusive scans of
-//                 the eleven lists' lengths, the section capacity check,
-//                 zeroing of the feed words
+//   k_feed_agg / k_feed_carry / k_feed_scan   the scan over chunks of 256
+//                 macroblocks (chunk aggregates in parallel, the chunks' carries
+//                 in order per frame, then the chunks in parallel again): the
+//                 table items' codes (segmented "previous value" scans for the
+//                 delta lists) and the exclusive scans of the eleven lists'
+//                 lengths, the section capacity check, zeroing of the feed words
 //   k_feed_write  one wave per macroblock again: codes OR-ed in at their offsets
 //   k_feed_copy   the used words (and the header) to the frame's mapped
 //                 pinned host buffer
@@ -167,22 +168,193 @@ __device__ __forceinline__ uint32_t item_code(int L, int value, int prev, int tb
 
 __device__ __forceinline__ bool delta_list(int L) { return L == kMvx || L == kMvy || L == kQuality; }
 
-constexpr int kScanT = 256, kScanW = kScanT / 64;  // small workgroups fit beside the persistent engine
+constexpr int kScanT = kFeedChunk, kScanW = kScanT / 64;  // small workgroups fit beside the persistent engine
+static_assert(kFeedChunkWords >= kLists + 9, "chunk record: 11 sums / offsets, 3 x (has, first, last)");
+constexpr int kDeltaLists[3] = {kMvx, kMvy, kQuality};
 
-// Phase 2: one 256-thread workgroup per frame walks the macroblocks in
-// chunks of 256 (one per thread, coalesced; a workgroup that small fits
-// beside the persistent engine's, so it runs in the slots a finishing launch
-// frees): the table items' codes, the
-// delta lists' previous values (segmented scans), and the exclusive scans of
-// all eleven lists' lengths with carries across chunks.  Offsets are stored
-// relative to their list's start; the list bases follow from the totals.
+// The table items and lengths of this thread's macroblock (chunk c, thread t)
+// and the delta lists' "previous present value" inside its wave
+// (segmented scans); shared by the aggregate and the final pass of the scan.
+struct ChunkItems {
+  bool valid;
+  BlockDesc d;
+  int val[kTabLists];
+  bool has[kTabLists];
+  int prev[3];  // 0x7FFFFFFF: no present item earlier in the wave
+  uint32_t len[kLists];
+};
+
+__device__ __forceinline__ void chunk_items(FA& a, const uint32_t* blen, int mbs, int mb, int lane, int hv_out[3],
+                                            int vv_out[3], ChunkItems& it) {
+  it.valid = mb < mbs;
+  if (it.valid) {
+    it.d = a.table[mb];
+  } else {
+    memset(&it.d, 0, sizeof(it.d));
+    it.d.block_type = kCopy;  // no items, no blocks
+  }
+#pragma unroll
+  for (int L = 0; L < kTabLists; L++) it.has[L] = it.valid && item(L, it.d, it.val[L]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int L = kDeltaLists[k];
+    int hv = it.has[L], vv = it.val[L];  // inclusive within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+      const int h2 = __shfl_up(hv, o), v2 = __shfl_up(vv, o);
+      if (lane >= o && !hv) hv = h2, vv = v2;
+    }
+    hv_out[k] = hv, vv_out[k] = vv;
+    const int he = __shfl_up(hv, 1), ve = __shfl_up(vv, 1);  // exclusive within the wave
+    it.prev[k] = lane > 0 && he ? ve : 0x7FFFFFFF;             // 0x7FFFFFFF: look further back
+  }
+#pragma unroll
+  for (int L = 0; L < kTabLists; L++) it.len[L] = 0;
+  it.len[kSecY] = it.valid ? blen[mb] + blen[mbs + mb] + blen[2 * (size_t)mbs + mb] + blen[3 * (size_t)mbs + mb] : 0;
+  it.len[kSecU] = it.valid ? blen[4 * (size_t)mbs + mb] : 0;
+  it.len[kSecV] = it.valid ? blen[5 * (size_t)mbs + mb] : 0;
+}
+
+__device__ __forceinline__ uint32_t* chunk_record(const FeedArgs& f, int slot, int mbs, int c) {
+  return f.scratch + (size_t)slot * f.scratch_stride + (size_t)kFeedScratchPerMB * mbs + (size_t)c * kFeedChunkWords;
+}
+
+// The scan of the table lists and sections (serialize.cpp:156-286) runs in
+// three passes over chunks of kFeedChunk macroblocks, so that the chunks of
+// a frame run in parallel (one workgroup per frame walking its 127 chunks of a
+// 4K frame took 0.83 ms of the gap between two engine launches):
+//   k_feed_agg    per chunk: each list's summed lengths, except the delta
+//                 lists' first present item (its code depends on the value
+//                 before the chunk), and that item's value and the chunk's
+//                 last present value;
+//   k_feed_carry  per frame: the chunks in order -- the first items'
+//                 lengths, each chunk's offset within every list and its
+//                 delta carries; the list bases, capacity check and header;
+//   k_feed_scan   per chunk: the items' codes and positions (as before, from
+//                 the chunk's carry-ins), and its share of zeroing the feed.
+__global__ __launch_bounds__(kScanT) void k_feed_agg(FeedArgs f) {
+  __shared__ uint32_t wsum[kScanW][kLists];
+  __shared__ int whas[kScanW][3], wval[kScanW][3], wfh[kScanW][3], wfv[kScanW][3];
+  FA& a = ((FA*)f.fa)[blockIdx.y];
+  const int slot = f.slot[blockIdx.y];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, mbs = a.wmb * a.hmb;
+  const int tbits = 31 - __clz(max(a.ring & 0xFF, 1));
+  const uint32_t* blen = f.scratch + (size_t)slot * f.scratch_stride;
+  const int mb = blockIdx.x * kScanT + t;
+  ChunkItems it;
+  int hv[3], vv[3];
+  chunk_items(a, blen, mbs, mb, lane, hv, vv, it);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int L = kDeltaLists[k];
+    const uint64_t b = __ballot(it.has[L]);  // the wave's first present item
+    const int fl = b ? (int)__ffsll((unsigned long long)b) - 1 : 0;
+    const int fv = __shfl(it.val[L], fl);
+    if (lane == 63) whas[w][k] = hv[k], wval[w][k] = vv[k], wfh[w][k] = b != 0, wfv[w][k] = fv;
+  }
+  __syncthreads();
+  bool first[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int L = kDeltaLists[k];
+    int pv = it.prev[k];
+    first[k] = false;
+    if (pv == 0x7FFFFFFF) {  // the last present value of an earlier wave of the chunk, if any
+      for (int i = w - 1; i >= 0; i--)
+        if (whas[i][k]) {
+          pv = wval[i][k];
+          break;
+        }
+      if (pv == 0x7FFFFFFF) first[k] = it.has[L];  // the chunk's first present item: done by k_feed_carry
+    }
+    if (it.has[L] && !first[k]) (void)item_code(L, it.val[L], pv, tbits, &it.len[L]);
+  }
+#pragma unroll
+  for (int L = 0; L < kTabLists; L++)
+    if (it.has[L] && !delta_list(L)) (void)item_code(L, it.val[L], 0, tbits, &it.len[L]);
+#pragma unroll
+  for (int L = 0; L < kLists; L++) {
+    const uint32_t x = wave_sum(it.len[L]);
+    if (lane == 0) wsum[w][L] = x;
+  }
+  __syncthreads();
+  uint32_t* rec = chunk_record(f, slot, mbs, blockIdx.x);
+  if (t < kLists) {
+    uint32_t s = 0;
+    for (int i = 0; i < kScanW; i++) s += wsum[i][t];
+    rec[t] = s;
+  } else if (t < kLists + 3) {  // per delta list: any present item, the first's value, the last's value
+    const int k = t - kLists;
+    int has = 0, fv = 0, lv = 0;
+    for (int i = 0; i < kScanW; i++) {
+      if (wfh[i][k] && !has) fv = wfv[i][k];
+      if (whas[i][k]) has = 1, lv = wval[i][k];
+    }
+    rec[kLists + k] = has, rec[kLists + 3 + k] = fv, rec[kLists + 6 + k] = lv;
+  }
+}
+
+// One wave per frame: lane L walks list L's chunk records in order (staged
+// through LDS 64 at a time), replacing each record's sums by the chunk's
+// offset within the list and, for the delta lists, its carry-in (any
+// present value before the chunk, and the last one).
+__global__ __launch_bounds__(64) void k_feed_carry(FeedArgs f) {
+  constexpr int kTile = 64;
+  __shared__ uint32_t tile[kTile * kFeedChunkWords];
+  FA& a = ((FA*)f.fa)[blockIdx.x];
+  const int slot = f.slot[blockIdx.x];
+  const int lane = threadIdx.x, mbs = a.wmb * a.hmb, nch = (mbs + kFeedChunk - 1) / kFeedChunk;
+  uint32_t* rec0 = chunk_record(f, slot, mbs, 0);
+  uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
+  const int k = lane == kMvx ? 0 : (lane == kMvy ? 1 : (lane == kQuality ? 2 : -1));
+  uint64_t run = 0;
+  int ch = 0, cv = 0;
+  for (int c0 = 0; c0 < nch; c0 += kTile) {
+    const int n = min(kTile, nch - c0);
+    for (int i = lane; i < n * kFeedChunkWords; i += 64) tile[i] = rec0[(size_t)c0 * kFeedChunkWords + i];
+    __syncthreads();
+    if (lane < kLists) {
+      for (int c = 0; c < n; c++) {
+        uint32_t* r = &tile[c * kFeedChunkWords];
+        uint32_t sum = r[lane];
+        if (k >= 0) {
+          const int has = (int)r[kLists + k], fv = (int)r[kLists + 3 + k], lv = (int)r[kLists + 6 + k];
+          if (has) sum += eg_len(se_val((int16_t)(fv - (ch ? cv : 0))));
+          r[kLists + k] = (uint32_t)ch, r[kLists + 3 + k] = (uint32_t)cv;  // carry-in
+          if (has) ch = 1, cv = lv;
+        }
+        r[lane] = (uint32_t)run;  // offsets within a list stay below 2^26 (else overflow, below)
+        run += sum;
+      }
+    }
+    __syncthreads();
+    for (int i = lane; i < n * kFeedChunkWords; i += 64) rec0[(size_t)c0 * kFeedChunkWords + i] = tile[i];
+    __syncthreads();
+  }
+  // list bases, capacity, header
+  uint64_t base = run;  // lane L: list L's total -> exclusive prefix over the lists
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(base, o);
+    if (lane >= o) base += y;
+  }
+  base -= run;
+  const uint64_t all = __shfl(base + run, kLists - 1);
+  const bool sec_over = lane >= kSecY && lane < kLists && run > kFeedCapacityBits;
+  const bool o = __ballot(sec_over) != 0 || all + 64 > (uint64_t)f.feed_stride * 32;
+  if (lane < kLists) hdr[4 + lane] = (uint32_t)base;
+  if (lane == 0) hdr[0] = (uint32_t)all, hdr[1] = (uint32_t)(all >> 32), hdr[2] = o ? 1u : 0u;
+}
+
+// Per chunk: the table items' codes and positions within their lists, and
+// the blocks' offsets within their sections, from the chunk's carry-ins
+// (k_feed_carry); then the chunk's share of zeroing the words k_feed_write
+// ORs into.
 __global__ __launch_bounds__(kScanT) void k_feed_scan(FeedArgs f) {
   __shared__ uint32_t wsum[kScanW][kLists];
   __shared__ int whas[kScanW][3], wval[kScanW][3];
-  __shared__ uint64_t carry_bits[kLists];
+  __shared__ uint32_t carry_bits[kLists];
   __shared__ int carry_has[3], carry_val[3];
-  FA& a = ((FA*)f.fa)[blockIdx.x];
-  const int slot = f.slot[blockIdx.x];
+  FA& a = ((FA*)f.fa)[blockIdx.y];
+  const int slot = f.slot[blockIdx.y];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, mbs = a.wmb * a.hmb;
   const int tbits = 31 - __clz(max(a.ring & 0xFF, 1));  // log2((uint8)R), serialize.cpp:179
   uint32_t* sc = f.scratch + (size_t)slot * f.scratch_stride;
@@ -190,121 +362,80 @@ __global__ __launch_bounds__(kScanT) void k_feed_scan(FeedArgs f) {
   uint32_t* tcode = sc + 6 * (size_t)mbs;     // [8][mbs]
   uint32_t* tpos = tcode + 8 * (size_t)mbs;   // [8][mbs]: len << 26 | offset in list
   uint32_t* boff = tpos + 8 * (size_t)mbs;    // [3][mbs]: offset of the MB's first block in its section
-  uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
-  if (t < kLists) carry_bits[t] = 0;
-  if (t < 3) carry_has[t] = 0, carry_val[t] = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < mbs; c0 += kScanT) {
-    const int mb = c0 + t;
-    const bool valid = mb < mbs;
-    BlockDesc d;
-    if (valid) {
-      d = a.table[mb];
-    } else {
-      memset(&d, 0, sizeof(d));
-      d.block_type = kCopy;  // no items, no blocks
-    }
-    // the delta lists' previous values: segmented "last present" scans
-    int val[kTabLists], prev[3];
-    bool has[kTabLists];
+  const uint32_t* hdr = f.hdr + (size_t)slot * kFeedHdrWords;
+  const uint32_t* rec = chunk_record(f, slot, mbs, blockIdx.x);
+  if (t < kLists) carry_bits[t] = rec[t];
+  if (t < 3) carry_has[t] = (int)rec[kLists + t], carry_val[t] = (int)rec[kLists + 3 + t];
+  const int mb = blockIdx.x * kScanT + t;
+  ChunkItems it;
+  int hv[3], vv[3];
+  chunk_items(a, blen, mbs, mb, lane, hv, vv, it);
 #pragma unroll
-    for (int L = 0; L < kTabLists; L++) has[L] = valid && item(L, d, val[L]);
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int L = k == 0 ? kMvx : (k == 1 ? kMvy : kQuality);
-      int hv = has[L], vv = val[L];  // inclusive within the wave
-      for (int o = 1; o < 64; o <<= 1) {
-        const int h2 = __shfl_up(hv, o), v2 = __shfl_up(vv, o);
-        if (lane >= o && !hv) hv = h2, vv = v2;
-      }
-      if (lane == 63) whas[w][k] = hv, wval[w][k] = vv;
-      const int he = __shfl_up(hv, 1), ve = __shfl_up(vv, 1);  // exclusive within the wave
-      prev[k] = lane > 0 && he ? ve : 0x7FFFFFFF;                // 0x7FFFFFFF: look further back
+  for (int k = 0; k < 3; k++)
+    if (lane == 63) whas[w][k] = hv[k], wval[w][k] = vv[k];
+  __syncthreads();  // whas / wval and the carry-ins complete
+  if (t < 3) {  // waves' carries, in order: the last present value before each wave
+    int h = carry_has[t], v = carry_val[t];
+    for (int i = 0; i < kScanW; i++) {
+      const int h2 = whas[i][t], v2 = wval[i][t];
+      whas[i][t] = h, wval[i][t] = v;
+      if (h2) h = 1, v = v2;
     }
-    // the lengths
-    uint32_t len[kLists], code[kTabLists];
-#pragma unroll
-    for (int L = 0; L < kTabLists; L++) len[L] = 0, code[L] = 0;
-    len[kSecY] = valid ? blen[mb] + blen[mbs + mb] + blen[2 * (size_t)mbs + mb] + blen[3 * (size_t)mbs + mb] : 0;
-    len[kSecU] = valid ? blen[4 * (size_t)mbs + mb] : 0;
-    len[kSecV] = valid ? blen[5 * (size_t)mbs + mb] : 0;
-    __syncthreads();  // whas / wval complete
-    if (t < 3) {  // waves' carries, in order: the last present value before each wave
-      int hv = carry_has[t], vv = carry_val[t];
-      for (int i = 0; i < kScanW; i++) {
-        const int h2 = whas[i][t], v2 = wval[i][t];
-        whas[i][t] = hv, wval[i][t] = vv;
-        if (h2) hv = 1, vv = v2;
-      }
-      carry_has[t] = hv, carry_val[t] = vv;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int L = k == 0 ? kMvx : (k == 1 ? kMvy : kQuality);
-      if (prev[k] == 0x7FFFFFFF) prev[k] = whas[w][k] ? wval[w][k] : 0;
-      if (has[L]) code[L] = item_code(L, val[L], prev[k], tbits, &len[L]);
-    }
-#pragma unroll
-    for (int L = 0; L < kTabLists; L++)
-      if (has[L] && !delta_list(L)) code[L] = item_code(L, val[L], 0, tbits, &len[L]);
-    // exclusive scans of the eleven lengths
-    uint32_t inc[kLists];
-#pragma unroll
-    for (int L = 0; L < kLists; L++) {
-      uint32_t x = len[L];
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-      }
-      inc[L] = x;
-      if (lane == 63) wsum[w][L] = x;
-    }
-    __syncthreads();
-    if (t < kLists) {  // wave prefixes, plus the running carry of the list
-      uint64_t s = carry_bits[t];
-      for (int i = 0; i < kScanW; i++) {
-        const uint32_t u = wsum[i][t];
-        wsum[i][t] = (uint32_t)s;  // offsets within a list stay below 2^26 (else overflow, below)
-        s += u;
-      }
-      carry_bits[t] = s;
-    }
-    __syncthreads();
-    if (valid) {
-#pragma unroll
-      for (int L = 0; L < kTabLists; L++) {
-        const uint32_t off = wsum[w][L] + inc[L] - len[L];
-        tcode[(size_t)L * mbs + mb] = code[L];
-        tpos[(size_t)L * mbs + mb] = has[L] ? (len[L] << 26) | (off & 0x3FFFFFFu) : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; k++) boff[(size_t)k * mbs + mb] = wsum[w][kSecY + k] + inc[kSecY + k] - len[kSecY + k];
-    }
-    __syncthreads();  // wsum / whas reused by the next chunk
-  }
-  // list bases, capacity, header; then zero the words the writer ORs into
-  __shared__ uint64_t all_bits;
-  __shared__ int over;
-  if (t == 0) {
-    uint64_t b = 0;
-    for (int L = 0; L < kLists; L++) {
-      hdr[4 + L] = (uint32_t)b;
-      b += carry_bits[L];
-    }
-    const bool o = carry_bits[kSecY] > kFeedCapacityBits || carry_bits[kSecU] > kFeedCapacityBits ||
-                   carry_bits[kSecV] > kFeedCapacityBits || b + 64 > (uint64_t)f.feed_stride * 32;
-    hdr[0] = (uint32_t)b;
-    hdr[1] = (uint32_t)(b >> 32);
-    hdr[2] = o ? 1u : 0u;
-    all_bits = b;
-    over = o;
   }
   __syncthreads();
-  if (over) return;  // the host codes this frame from its planes
+  uint32_t code[kTabLists];
+#pragma unroll
+  for (int L = 0; L < kTabLists; L++) code[L] = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int L = kDeltaLists[k];
+    if (it.prev[k] == 0x7FFFFFFF) it.prev[k] = whas[w][k] ? wval[w][k] : 0;
+    if (it.has[L]) code[L] = item_code(L, it.val[L], it.prev[k], tbits, &it.len[L]);
+  }
+#pragma unroll
+  for (int L = 0; L < kTabLists; L++)
+    if (it.has[L] && !delta_list(L)) code[L] = item_code(L, it.val[L], 0, tbits, &it.len[L]);
+  // exclusive scans of the eleven lengths
+  uint32_t inc[kLists];
+#pragma unroll
+  for (int L = 0; L < kLists; L++) {
+    uint32_t x = it.len[L];
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    inc[L] = x;
+    if (lane == 63) wsum[w][L] = x;
+  }
+  __syncthreads();
+  if (t < kLists) {  // wave prefixes, plus the chunk's offset within the list
+    uint32_t s = carry_bits[t];
+    for (int i = 0; i < kScanW; i++) {
+      const uint32_t u = wsum[i][t];
+      wsum[i][t] = s;
+      s += u;
+    }
+  }
+  __syncthreads();
+  if (it.valid) {
+#pragma unroll
+    for (int L = 0; L < kTabLists; L++) {
+      const uint32_t off = wsum[w][L] + inc[L] - it.len[L];
+      tcode[(size_t)L * mbs + mb] = code[L];
+      tpos[(size_t)L * mbs + mb] = it.has[L] ? (it.len[L] << 26) | (off & 0x3FFFFFFu) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      boff[(size_t)k * mbs + mb] = wsum[w][kSecY + k] + inc[kSecY + k] - it.len[kSecY + k];
+  }
+  // this chunk's share of the words the writer ORs into (none on overflow:
+  // the host codes that frame from its planes)
+  if (hdr[2]) return;
+  const uint64_t all_bits = (uint64_t)hdr[0] | ((uint64_t)hdr[1] << 32);
+  const uint64_t words = (all_bits + 31) / 32 + 1, per = (words + gridDim.x - 1) / gridDim.x;
   uint32_t* feed = f.feed + (size_t)slot * f.feed_stride;
-  const uint64_t words = (all_bits + 31) / 32 + 1;
-  for (uint64_t i = t; i < words; i += kScanT) feed[i] = 0;
+  const uint64_t w0 = (uint64_t)blockIdx.x * per, w1 = min(words, w0 + per);
+  for (uint64_t i = w0 + t; i < w1; i += kScanT) feed[i] = 0;
 }
 
 // Words an 8x8 block's codes can span: ue(65) (13 bits) + 64 codes of at
@@ -414,7 +545,10 @@ __global__ __launch_bounds__(256) void k_feed_copy(FeedArgs f) {
 hipError_t launch_precode(const FeedArgs& f, int mbs, hipStream_t s) {
   const dim3 blocks((mbs + 3) / 4, f.nframes);
   hipLaunchKernelGGL(k_feed_len, blocks, dim3(256), 0, s, f);
-  hipLaunchKernelGGL(k_feed_scan, dim3(f.nframes), dim3(kScanT), 0, s, f);
+  const int nch = (mbs + kFeedChunk - 1) / kFeedChunk;
+  hipLaunchKernelGGL(k_feed_agg, dim3(nch, f.nframes), dim3(kScanT), 0, s, f);
+  hipLaunchKernelGGL(k_feed_carry, dim3(f.nframes), dim3(64), 0, s, f);
+  hipLaunchKernelGGL(k_feed_scan, dim3(nch, f.nframes), dim3(kScanT), 0, s, f);
   hipLaunchKernelGGL(k_feed_write, blocks, dim3(256), 0, s, f);
   hipLaunchKernelGGL(k_feed_copy, dim3(64, f.nframes), dim3(256), 0, s, f);
   return hipGetLastError();
