@@ -102,10 +102,44 @@ __device__ __forceinline__ int run_of(int c) {
   return nz ? 64 - __clzll(nz) : 0;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// Wave scans by DPP (gfx9 row shifts and row broadcasts: six dependent VALU
+// steps instead of six LDS permutes).  dpp_src: lane i's source value, 0 where
+// the control selects none (bound_ctrl off: the old value, 0, stays).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, false);
 }
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += dpp_src<0x111, 0xF>(x);  // row_shr:1
+  x += dpp_src<0x112, 0xF>(x);  // row_shr:2
+  x += dpp_src<0x114, 0xF>(x);  // row_shr:4
+  x += dpp_src<0x118, 0xF>(x);  // row_shr:8
+  x += dpp_src<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+  x += dpp_src<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+  return x;
+}
+// The wave's total (uniform).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
+}
+// Segmented "last present value" scan (inclusive): (h, v) of the latest lane
+// <= this one with h set.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void last_step(int& h, int& v) {
+  const int h2 = (int)dpp_src<kCtrl, kRowMask>((uint32_t)h), v2 = (int)dpp_src<kCtrl, kRowMask>((uint32_t)v);
+  if (!h) h = h2, v = v2;
+}
+__device__ __forceinline__ void wave_last_present(int& h, int& v) {
+  last_step<0x111, 0xF>(h, v);
+  last_step<0x112, 0xF>(h, v);
+  last_step<0x114, 0xF>(h, v);
+  last_step<0x118, 0xF>(h, v);
+  last_step<0x142, 0xA>(h, v);
+  last_step<0x143, 0xC>(h, v);
+}
+// Lane i - 1's value (0 on lane 0): wave_shr:1.
+__device__ __forceinline__ int wave_prev(int v) { return (int)dpp_src<0x138, 0xF>((uint32_t)v); }
 
 // Phase 1: one wave per macroblock, the bits of its six blocks.
 __global__ __launch_bounds__(256) void k_feed_len(FeedArgs f) {
@@ -199,12 +233,9 @@ __device__ __forceinline__ void chunk_items(FA& a, const uint32_t* blen, int mbs
   for (int k = 0; k < 3; k++) {
     const int L = kDeltaLists[k];
     int hv = it.has[L], vv = it.val[L];  // inclusive within the wave
-    for (int o = 1; o < 64; o <<= 1) {
-      const int h2 = __shfl_up(hv, o), v2 = __shfl_up(vv, o);
-      if (lane >= o && !hv) hv = h2, vv = v2;
-    }
+    wave_last_present(hv, vv);
     hv_out[k] = hv, vv_out[k] = vv;
-    const int he = __shfl_up(hv, 1), ve = __shfl_up(vv, 1);  // exclusive within the wave
+    const int he = wave_prev(hv), ve = wave_prev(vv);  // exclusive within the wave
     it.prev[k] = lane > 0 && he ? ve : 0x7FFFFFFF;             // 0x7FFFFFFF: look further back
   }
 #pragma unroll
@@ -399,11 +430,7 @@ __global__ __launch_bounds__(kScanT) void k_feed_scan(FeedArgs f) {
   uint32_t inc[kLists];
 #pragma unroll
   for (int L = 0; L < kLists; L++) {
-    uint32_t x = it.len[L];
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
+    const uint32_t x = wave_incl_sum(it.len[L]);
     inc[L] = x;
     if (lane == 63) wsum[w][L] = x;
   }
@@ -477,13 +504,9 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
     const int run = run_of(c[b]);
     const uint32_t val = se_val(c[b]);
     const uint32_t len = lane < run ? eg_len(val) : 0u;
-    uint32_t x = len;  // inclusive prefix of the lane lengths
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
+    const uint32_t x = wave_incl_sum(len);  // inclusive prefix of the lane lengths
     const uint32_t ul = eg_len((uint32_t)run + 1u);
-    const uint64_t end = pos + ul + __shfl(x, 63);
+    const uint64_t end = pos + ul + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     const uint64_t w0 = pos >> 5;
     const int nw = (int)(((end + 31) >> 5) - w0);  // <= kBlockWords
     for (int i = lane; i < nw; i += 64) sw[i] = 0;
