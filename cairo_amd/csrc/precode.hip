@@ -70,20 +70,41 @@ __device__ __forceinline__ void or_bits(uint32_t* w, uint64_t p, uint32_t code, 
 // zig-zag coefficient of each (lane k = scan position k), with the delta DC
 // on lane 0 (serialize.cpp:35-123: the left neighbour's block at x - 8, or
 // the one above at y - 8 in the first column; stale output_cache values of
-// copy macroblocks included).  All six loads are issued together.
-__device__ __forceinline__ void mb_coefs(FA& a, int mb, int lane, int c[6]) {
+// copy macroblocks included).
+// Lanes 0..47 load the macroblock's 768 bytes as
+// 16-byte rows (luma 16 rows x 2 halves, then 8 U and 8 V rows) into the
+// wave's buffer (luma 16x16, U 8x8, V 8x8), then every lane reads its
+// zig-zag element of each block: one wide load per lane instead of six
+// scattered 2-byte loads.
+__device__ __forceinline__ void mb_coefs(FA& a, int mb, int lane, int16_t* buf, int c[6]) {
   const int mx = mb % a.wmb, my = mb / a.wmb;
-  const int r = kZig[lane], ry = r >> 3, rx = r & 7;
-  const int16_t* y = a.coef.y;
-  const int16_t* u = a.coef.u;
-  const int16_t* v = a.coef.v;
   const int w = a.wa, cw = a.wa >> 1;
   const int x0 = 16 * mx, y0 = 16 * my, cx = 8 * mx, cy = 8 * my;
+  if (lane < 48) {
+    const int16_t* src;
+    int dst;
+    if (lane < 32) {
+      src = a.coef.y + (size_t)(y0 + (lane >> 1)) * w + x0 + 8 * (lane & 1);
+      dst = (lane >> 1) * 16 + 8 * (lane & 1);
+    } else {
+      const int r = lane & 7;
+      src = (lane < 40 ? a.coef.u : a.coef.v) + (size_t)(cy + r) * cw + cx;
+      dst = (lane < 40 ? 256 : 320) + 8 * r;
+    }
+    *(uint4*)&buf[dst] = *(const uint4*)src;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int r = kZig[lane], ry = r >> 3, rx = r & 7;
 #pragma unroll
-  for (int b = 0; b < 4; b++) c[b] = y[(size_t)(y0 + 8 * (b >> 1) + ry) * w + x0 + 8 * (b & 1) + rx];
-  c[4] = u[(size_t)(cy + ry) * cw + cx + rx];
-  c[5] = v[(size_t)(cy + ry) * cw + cx + rx];
+  for (int b = 0; b < 4; b++) c[b] = buf[(8 * (b >> 1) + ry) * 16 + 8 * (b & 1) + rx];
+  c[4] = buf[256 + r];
+  c[5] = buf[320 + r];
   if (lane == 0) {
+    const int16_t* y = a.coef.y;
+    const int16_t* u = a.coef.u;
+    const int16_t* v = a.coef.v;
     const int16_t dy = mx > 0 ? y[(size_t)y0 * w + x0 - 8] : (my > 0 ? y[(size_t)(y0 - 8) * w + x0] : 0);
     const int16_t du = mx > 0 ? u[(size_t)cy * cw + cx - 8] : (my > 0 ? u[(size_t)(cy - 8) * cw + cx] : 0);
     const int16_t dv = mx > 0 ? v[(size_t)cy * cw + cx - 8] : (my > 0 ? v[(size_t)(cy - 8) * cw + cx] : 0);
@@ -152,8 +173,9 @@ __global__ __launch_bounds__(256) void k_feed_len(FeedArgs f) {
     if (lane < 6) blen[(size_t)lane * mbs + mb] = 0;
     return;
   }
+  __shared__ __attribute__((aligned(16))) int16_t cbuf[4][384];
   int c[6];
-  mb_coefs(a, mb, lane, c);
+  mb_coefs(a, mb, lane, cbuf[threadIdx.x >> 6], c);
   uint32_t mine = 0;
 #pragma unroll
   for (int b = 0; b < 6; b++) {
@@ -493,9 +515,10 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
   // its bit range belong to it alone (plain stores); only its first and last
   // word are shared with the neighbouring blocks (global atomic OR).
   __shared__ uint32_t stage[4][kBlockWords];
+  __shared__ __attribute__((aligned(16))) int16_t cbuf[4][384];
   uint32_t* sw = stage[threadIdx.x >> 6];
   int c[6];
-  mb_coefs(a, mb, lane, c);
+  mb_coefs(a, mb, lane, cbuf[threadIdx.x >> 6], c);
   uint64_t pos = (uint64_t)hdr[4 + kSecY] + boff[mb];
 #pragma unroll
   for (int b = 0; b < 6; b++) {
