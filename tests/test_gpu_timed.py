@@ -67,9 +67,9 @@ def test_timed_4k_many_launches(orc, cairo):
     _run_batched(orc, cairo, 3840, 2160, 4, 16, 44, 10, outputs=cairo.OUT_FEED, device_frames=True)
 
 
-def _golden_stream_run(cairo, config, frames, batch=0):
+def _golden_stream_run(cairo, config, frames, batch=0, content="band4"):
     """bench.py's timed leg exactly (its run_hot_path, FrameStore and record
-    hashing): `frames` band4 frames resident in HBM, the library's default
+    hashing): `frames` frames of `content` (bench.content_frame) resident in HBM, the library's default
     frames per launch, feed outputs, up to `stages` in flight; every frame's
     record hash against tests/golden/stream_<config>_*.json (the oracle's, made
     off-box), so long runs need no oracle time here."""
@@ -78,7 +78,7 @@ def _golden_stream_run(cairo, config, frames, batch=0):
     import bench
 
     w, h, ring, q, _ = bench.CONFIGS[config]
-    g = bench.golden_stream(config, "band4", q, ring)
+    g = bench.golden_stream(config, content, q, ring)
     assert g is not None and g["frames"] >= frames, f"golden stream for {config} has too few frames"
     hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime the library uses
     size = w * h * 3
@@ -86,7 +86,7 @@ def _golden_stream_run(cairo, config, frames, batch=0):
     assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(frames * size)) == 0
     try:
         for t in range(frames):
-            f = cairo.make_band4(w, h, t)
+            f = bench.content_frame(content, w, h, t)
             assert hip.hipMemcpy(ctypes.c_void_p(dev.value + t * size), f.ctypes.data_as(ctypes.c_void_p),
                                  ctypes.c_size_t(size), 1) == 0
         ctx = cairo.Context(w, h, ring)
@@ -123,6 +123,17 @@ def test_timed_1080p_golden_160(cairo):
 def test_timed_720p_golden_200(cairo):
     """configs[1] (q=16, R=2), 200 frames at 32 per launch, against the golden stream."""
     _golden_stream_run(cairo, "720p", 200)
+
+
+@pytest.mark.parametrize("content", ["noise", "static"])
+def test_timed_4k_content_golden_160(cairo, content):
+    """SURVEY §8(d)'s stress content at the bench's configuration, 160
+    frames (five launches of 32): noise (every macroblock searched and coded,
+    no copy exits) and a static scene (copy chains: each macroblock's
+    coefficients carried from the previous frame's output_cache, the case the
+    coefficient drain before the info granule protects), against their
+    golden streams."""
+    _golden_stream_run(cairo, "4k", 160, content=content)
 
 
 def test_timed_4k_both_outputs(orc, cairo):
