@@ -319,13 +319,13 @@ constexpr int kPrioFrameMBs = 4000;
 // L2.  Correctness does not rest on the placement: labels partition the block
 // indices, each label has workers of both pools, and each label's queue is a
 // subsequence of the task order (deadlock freedom as for one queue).
-// 4K A/B (DESIGN §4.3): 5387-5391 -> 5483-5486 Mpix/s, engine reads -29 %;
+// 4K A/B (DESIGN §4.2, round 3): 5387-5391 -> 5483-5486 Mpix/s, engine reads -29 %;
 // at 1080p (68 rows) -1.2 %, so not below kBandMinRows.
 constexpr int kLabels = 8;
 constexpr int kBandMinRows = 100;
 constexpr int kBandPools = 3;  // bit 0: the helpers' queues are per label, bit 1: the coders'
 // Contiguous bands of hmb / kLabels rows (rotating 4- or 8-row bands read
-// fewer bytes but ran 0.4-0.8 % slower).
+// fewer bytes but ran 0.4-0.8 % slower: profiles/r04/band_traffic_4k.json, ab_4k_k.txt).
 __host__ __device__ inline int task_label(int frame, int row, int hmb) {
   (void)frame;
   return row * kLabels / hmb;

@@ -2498,7 +2498,8 @@ __device__ __forceinline__ void row_helper(FA& a0, int r, HelperLds& L, int* fla
     }
     // level 1 of the group's window in the previous frame; deblock meanwhile
     // (leaving the chunks to the catch-up after the group's records instead
-    // measured neutral)
+    // measured neutral in round 4; catch-ups between the older references'
+    // searches too, in round 5)
     helper_wait(a, 1, r, min(r + 2, a.hmb - 1), inter_need_cols(a, g, 1), L.db, st, flag);
     if (is) is[1] = __builtin_amdgcn_s_memrealtime();
     trace(tr, 3, 50);
