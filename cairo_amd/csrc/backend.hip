@@ -177,13 +177,9 @@ struct cairo_ctx {
   uint32_t* feed_scratch = nullptr;  // [stages][feed_scratch_words(mbs)]
   uint32_t* feed_host = nullptr;  // mapped pinned [stages][kFeedHdrWords + feed_words]
   hipStream_t fs = nullptr;       // synchronous coefficient fetches (a frame whose feed overflowed)
-  // The precode runs on a stream of its own after each launch, filling the
-  // gaps the persistent engine leaves; on the launch stream it would hold the
-  // next launch back (A/B at 4K: 3583 vs 3768 Mpix/s).
-  hipStream_t ps = nullptr;
-  hipEvent_t pre_done[kSyncAreas] = {};
-  hipEvent_t kernel_end[kSyncAreas] = {};  // (precode on its own stream) the engine kernel of that area's launch ended
-  bool ps_own = getenv("CAIRO_PRECODE_OWN_STREAM") != nullptr;  // A/B switch
+  // (The precode runs on the launch's stream, between its kernel and the
+  // launch two ahead: on a stream of its own its kernels took the slots the
+  // next launch's workers need, -2 to -5 % at 4K)
   bool sys = false;           // a member is another process or device: system-scope hand-offs
   int32_t *sync = nullptr;
   int32_t* sticky = nullptr;  // TimeoutInfo words (kernels.h), cleared only by zero_state
@@ -412,7 +408,6 @@ void free_ctx(cairo_ctx* c) {
   if (c->ks) (void)hipStreamSynchronize(c->ks);
   if (c->ks2) (void)hipStreamSynchronize(c->ks2);
   if (c->cs) (void)hipStreamSynchronize(c->cs);
-  if (c->ps) (void)hipStreamSynchronize(c->ps);  // the precode writes into feed_host
   for (auto& s : c->st) {
     if (s.table) (void)hipHostFree(s.table);
     if (s.coef) (void)hipHostFree(s.coef);
@@ -434,11 +429,6 @@ void free_ctx(cairo_ctx* c) {
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
   if (c->feed_host) (void)hipHostFree(c->feed_host);
   if (c->fs) (void)hipStreamDestroy(c->fs);
-  for (auto& ev : c->pre_done)
-    if (ev) (void)hipEventDestroy(ev);
-  for (auto& ev : c->kernel_end)
-    if (ev) (void)hipEventDestroy(ev);
-  if (c->ps) (void)hipStreamDestroy(c->ps);
   if (c->trace_host) (void)hipHostFree(c->trace_host);
   leave_group(c);
   for (int16_t* q : c->coef)
@@ -635,17 +625,8 @@ int flush(cairo_ctx* c) {
   if (tb) CK(hipEventRecord(tb->ev[2], st));
   CK(launch_engine(e, st));
   // the launch ends when its workers find no task left; its batch is done
-  // when every task has finished (the next launch's workers may run the last).
-  // With the precode on a stream of its own the wait for that runs there too,
-  // so that the launch two ahead on this stream starts when this kernel ends,
-  // not after the previous launch's last tasks and the precode.
-  const bool own = c->ps_own && c->ps;
-  hipStream_t bst = own ? c->ps : st;
-  if (own) {
-    CK(hipEventRecord(c->kernel_end[area], st));
-    CK(hipStreamWaitEvent(c->ps, c->kernel_end[area], 0));
-  }
-  CK(launch_batch_wait(e.sync, 2 * rows, c->sticky, bst));
+  // when every task has finished (the next launch's workers may run the last)
+  CK(launch_batch_wait(e.sync, 2 * rows, c->sticky, st));
   c->prev_fa = fd;
   for (int k = 0; k < 2; k++) c->prev_order[k] = e.order[k], c->prev_seg[k] = e.seg[k];
   c->prev_sync = e.sync;
@@ -659,9 +640,7 @@ int flush(cairo_ctx* c) {
   }
   const int last = c->pend[e.nframes - 1].slot;
   const uint32_t last_epoch = c->pend[e.nframes - 1].epoch;
-  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), bst));
-  hipStream_t pst = bst;
-  if (own) CK(hipEventRecord(c->batch_end[area], bst));
+  if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
   if (c->outputs & CAIRO_OUT_FEED) {  // the entropy precode, straight into mapped host memory
     FeedArgs fa;
     memset(&fa, 0, sizeof(fa));
@@ -685,19 +664,14 @@ int flush(cairo_ctx* c) {
       fa.err_host[i] = c->pend[i].decode ? nullptr : s.err_dev;
     }
     fa.table_words = (int)(c->mbs * sizeof(BlockDesc) / sizeof(uint4));
-    CK(launch_precode(fa, (int)c->mbs, pst));
+    CK(launch_precode(fa, (int)c->mbs, st));
   }
-  if (!own) CK(hipEventRecord(c->batch_end[area], st));
+  CK(hipEventRecord(c->batch_end[area], st));
   // the copy stream carries D2H copies only with the coefficient planes; in
   // feed-only mode it carries the host-RGB uploads (submit), which must not
   // queue behind the launches in flight
   if (c->outputs & CAIRO_OUT_COEF) {
-    if (own && (c->outputs & CAIRO_OUT_FEED)) {
-      CK(hipEventRecord(c->pre_done[area], c->ps));
-      CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
-    } else {
-      CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
-    }
+    CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
   }
   // outputs for the host entropy stage: with the feed, the precode's last
   // kernel (k_feed_copy) has written each frame's feed, block table and
@@ -719,7 +693,7 @@ int flush(cairo_ctx* c) {
       CK(hipMemcpyAsync(s.coef, coef_base(c, slot), c->plane_elems * 2, hipMemcpyDeviceToHost, c->cs));
       CK(hipEventRecord(s.d2h_done, c->cs));
     } else {
-      CK(hipEventRecord(s.d2h_done, pst));
+      CK(hipEventRecord(s.d2h_done, st));
     }
     s.launched = true;
   }
@@ -809,7 +783,6 @@ int sync_all(cairo_ctx* c) {
   CK(hipStreamSynchronize(c->ks));
   CK(hipStreamSynchronize(c->ks2));
   CK(hipStreamSynchronize(c->cs));
-  if (c->ps) CK(hipStreamSynchronize(c->ps));
   if (c->us) CK(hipStreamSynchronize(c->us));
   return kSuccess;
 }
@@ -1315,11 +1288,6 @@ int cairo_ctx_set_outputs(cairo_ctx* c, int outputs) {
     }
     c->feed_words = words;
     c->feed_dev = dev, c->feed_hdr = hdr, c->feed_scratch = scratch, c->feed_host = host;
-    if (c->ps_own && !c->ps) {  // (the A/B variant: each stream takes a hardware queue)
-      CK(hipStreamCreateWithFlags(&c->ps, hipStreamNonBlocking));
-      for (auto& ev : c->pre_done) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      for (auto& ev : c->kernel_end) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    }
   }
   c->outputs = outputs;
   return kSuccess;
