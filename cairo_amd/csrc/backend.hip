@@ -529,7 +529,8 @@ int flush(cairo_ctx* c) {
   // launch takes at most half of the engine's resident
   // workgroup slots (CUs x occupancy, measured at create: 256 x 3 = 768 on a
   // full MI355X), so two launches are always co-resident.  Every row has a
-  // coder task and a helper (inter search + deblock) task: two pools.  The pools are shared: launch b's workers take b-1's
+  // coder task and a helper (inter search + deblock) task: two pools.  The
+  // pools are shared: launch b's workers take b-1's
   // remaining tasks first (all of them are older), so b-1's tail is not left
   // to b-1's own workers; a batch is complete when its finished-task count
   // says so (k_batch_wait), not when its launch ends.
