@@ -525,6 +525,11 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
     if (b == 4) pos = (uint64_t)hdr[4 + kSecU] + boff[(size_t)mbs + mb];
     if (b == 5) pos = (uint64_t)hdr[4 + kSecV] + boff[2 * (size_t)mbs + mb];
     const int run = run_of(c[b]);
+    if (run == 0) {  // (wave-uniform) an all-zero block is the one-bit ue(1): one atomic, no staging
+      if (lane == 0) or_bits(feed, pos, 1u, 1u);
+      pos += 1;
+      continue;
+    }
     const uint32_t val = se_val(c[b]);
     const uint32_t len = lane < run ? eg_len(val) : 0u;
     const uint32_t x = wave_incl_sum(len);  // inclusive prefix of the lane lengths
