@@ -16,7 +16,15 @@ CPP_SRCS = $(SRC)/entropy.cpp $(SRC)/bitstream.cpp $(SRC)/encoder.cpp $(SRC)/dec
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
 HDRS     = $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
 
-all: $(LIB) $(ORACLE) $(API_BIN)
+HOP_BIN  = tools/bin/hop_latency
+
+all: $(LIB) $(ORACLE) $(API_BIN) $(HOP_BIN)
+
+# Hand-off latency micro-benchmark: one hop of the progress-word
+# protocol between two workgroups, in one process or across two.
+$(HOP_BIN): tools/hop_latency.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -63,6 +71,6 @@ check-knobs:
 	@echo "check-knobs: every build switch compiles; CAIRO_ATTR_SKIP is refused in product builds"
 
 clean:
-	rm -rf build $(LIB) $(ORACLE) $(API_BIN)
+	rm -rf build $(LIB) $(ORACLE) $(API_BIN) $(HOP_BIN)
 
 .PHONY: all clean check-knobs

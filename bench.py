@@ -640,8 +640,10 @@ def main():
         exact["frames_checked"] = hp.get("timed_frames_checked", 0)  # timed frames, against the golden hashes
         exact["timed_frames"] = timed_frames
         exact["mismatches"] = bad
-        exact["bit_exact"] = bad == 0 and bool(exact["frames_checked"] == timed_frames or
-                                               ("oracle_sample" in exact and not golden))
+        # true only when every timed frame was compared; a run without a golden
+        # stream (only the oracle's live sample of warm-up frames) is unverified
+        exact["verified"] = exact["frames_checked"] == timed_frames
+        exact["bit_exact"] = False if bad else (True if exact["verified"] else None)
         exact["what"] = ("every frame of the timed context (warm-up and timed, same launches) and of the end-to-end "
                          "pipeline: the GPU feed / payload arithmetic-coded on host threads after the timed region, "
                          "the frame's stream record hashed (FNV-1a-64, header byte 7 and tail bits masked) and "
@@ -650,7 +652,8 @@ def main():
     if world > 1:
         allx = [None] * world
         dist.all_gather_object(allx, exact)
-        exact = {"ranks": allx, "bit_exact": all(x and x.get("bit_exact") for x in allx),
+        vals = [(x or {}).get("bit_exact") for x in allx]
+        exact = {"ranks": allx, "bit_exact": False if False in vals else (None if None in vals else True),
                  "frames_checked": sum((x or {}).get("frames_checked", 0) for x in allx),
                  "what": "every rank's own replica stream, every frame, against the golden hashes"}
     result["bit_exact"] = exact
@@ -817,7 +820,8 @@ def single_stream(cairo_amd, frame_ptr, a, w, h, ring, q, batch, warm, timed, ba
             ex["frames_checked"] = sum(g["timed_frames_checked"] for g in gchecks)
             bad += sum(g["mismatches"] for g in gchecks)
         ex["mismatches"] = bad
-        ex["bit_exact"] = bad == 0 and (ex.get("frames_checked") == timed or a.no_verify or not all(gchecks))
+        ex["verified"] = ex.get("frames_checked") == timed
+        ex["bit_exact"] = False if bad else (True if ex["verified"] else None)
         out["bit_exact"] = ex
     return out
 

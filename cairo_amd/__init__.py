@@ -280,7 +280,9 @@ class Context:
                    "helper_search", "helper_catchup", "helper_dequeue", "helper_chunks",
                    "win_bytes", "win_spec_unused_bytes", "zero_mv_bytes", "gran_poll_bytes", "rec_poll_bytes",
                    "win_stages", "searched_tasks", "inter_tasks", "coder_xform", "coder_publish", "coder_drain",
-                   "coder_vm0", "coder_records", "coder_prebarrier", "coder_store_tail")
+                   "coder_vm0", "coder_records", "coder_prebarrier", "coder_store_tail",
+                   "search_eval", "search_barrier", "search_select", "subpel_eval", "subpel_barrier",
+                   "subpel_select")
 
     def read_acct(self, reset: bool = False) -> dict:
         """Engine time accounting (set_debug(32) on a CAIRO_ACCT=1 build): 10 ns

@@ -1123,7 +1123,27 @@ static const char* timeout_kind_name(int k) {
 
 // A frame found the context's timeout words set: say on stderr which wait
 // gave up first, and keep the words for cairo_ctx_timeout_info.
-static void report_timeout_host(cairo_ctx* c, const int32_t* w, uint32_t index) {
+// w is a copy the host took without ordering between the words (a D2H copy,
+// or k_feed_copy's relaxed reads in the mapped stage) while a launch may still
+// have been writing the record.  The record's kind is stored last, with a
+// system-scope release (report_timeout in kernels.hip), so once a read has
+// seen the kind, every word of the record was visible before it: a second
+// read of the device words, started now, returns the whole record.
+// fs: a stream for that read (nullptr: the context's fetch stream, made under
+// mu, which the caller must not hold).
+static void report_timeout_host(cairo_ctx* c, const int32_t* seen, uint32_t index, hipStream_t fs = nullptr) {
+  int32_t w[TimeoutInfo::kWords];
+  memcpy(w, seen, sizeof(w));
+  {
+    if (!fs) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (!c->fs) (void)hipStreamCreateWithFlags(&c->fs, hipStreamNonBlocking);
+      fs = c->fs;
+    }
+    if (fs && hipMemcpyAsync(w, c->sticky, sizeof(w), hipMemcpyDeviceToHost, fs) == hipSuccess)
+      (void)hipStreamSynchronize(fs);
+    if (!w[TimeoutInfo::kKind]) memcpy(w, seen, sizeof(w));  // (a reset in between: keep what was seen)
+  }
   {
     std::lock_guard<std::mutex> lk(c->tmu);
     memcpy(c->timeout, w, sizeof(c->timeout));
@@ -1247,7 +1267,7 @@ int cairo_ctx_decode_frame(cairo_ctx* c, const uint8_t* table, const int16_t* co
       r = fail(hipMemcpyAsync(rgb, drgb, (size_t)c->w * c->h * 3, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     if (r == kSuccess) r = fail(hipStreamSynchronize(st), "hipStreamSynchronize");
     if (r == kSuccess && s.err[TimeoutInfo::kKind]) {
-      report_timeout_host(c, s.err, index);
+      report_timeout_host(c, s.err, index, st);  // (mu held: the launch stream, idle now)
       r = kHardwareFail;
     }
   }

@@ -112,7 +112,7 @@ enum TimeoutKind : int32_t {
 #ifndef CAIRO_ACCT
 #define CAIRO_ACCT 0
 #endif
-constexpr int kAcctShards = 64, kAcctWords = 32;
+constexpr int kAcctShards = 64, kAcctWords = 40;
 struct Acct {
   // row coders
   static constexpr int kCoderTasks = 0, kCoderTotal = 1, kCoderGroupWait = 2, kCoderWindow = 3, kCoderSearch = 4,
@@ -131,6 +131,11 @@ struct Acct {
   // records and predictions issued inside a group, the barrier
   static constexpr int kCoderVm0 = 27, kCoderRecords = 28, kCoderPreBarrier = 29;
   static constexpr int kCoderStoreTail = 30;  // CAIRO_ACCT_STORE_TAIL diagnostic builds
+  // inside the intra search (thread 0's wave, summed over a macroblock's
+  // integer stages / its sub-pel step): candidate evaluation and the result
+  // stores to LDS, the barrier, the LDS reads and the ordered replay
+  static constexpr int kSrchEval = 31, kSrchBarrier = 32, kSrchSelect = 33, kSubEval = 34, kSubBarrier = 35,
+                       kSubSelect = 36;
 };
 
 // Frames per engine launch.

@@ -227,8 +227,10 @@ __device__ __attribute__((noinline)) void report_timeout(int32_t* err, int32_t* 
     return;  // an earlier timeout is the one reported
   const int32_t w[8] = {(int32_t)epoch, index, row, member, need, on, (int32_t)(uint32_t)seen, (int32_t)(seen >> 32)};
   for (int k = 0; k < 8; k++) __hip_atomic_store(sticky + 1 + k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the kind last: readers (k_feed_copy, the host's D2H, cairo_ctx_timeout_info)
-  // take a set kind as the record's completion
+  // the kind last, with a system-scope release: a reader that acquire-loads
+  // the kind first (k_feed_copy) sees the whole record; the host's copies,
+  // which have no order between the words, only learn from the kind that the
+  // record exists and read it again (backend.hip report_timeout_host)
   __hip_atomic_store(sticky + TimeoutInfo::kKind, kind, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void report_timeout(FA& a, int kind, int row, int need, int on, uint64_t seen) {
@@ -1986,21 +1988,20 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
     }
     for (int bx = 0; bx < a0.wmb; bx++) {
       FA* ap = opaque_view(&a0);
-#define a (*ap)
-      const int px = bx * kMB, mb = by * a.wmb + bx;
+      const int px = bx * kMB, mb = by * ap->wmb + bx;
       trace(tr, 1, bx);
-      trace(tr, 2, (int)a.epoch * 1000 + by);
-      stamp(a, mb, 0);
-      if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
+      trace(tr, 2, (int)ap->epoch * 1000 + by);
+      stamp(*ap, mb, 0);
+      if (ap->stamps && tid == 0) ap->stamps[(size_t)mb * kStampPhases + 10] = __builtin_amdgcn_s_memtime();
       // The row above's fresh column block (bx+2, by-1): its first granule
       // load is issued before the group-start wait below, so that a granule
       // already there costs no round trip after it (the tag is the flag: a
       // 64-bit load needs no acquire).
       // macroblock bx+1's source into LDS, in flight with the fresh granule
       // load below, whose wait covers it (the buffer was last read in bx-1)
-      if (!kDecode && bx + 1 < a.wmb) src_dma(a, bx + 1, by, L.src[(bx + 1) & 1]);
-      const bool fresh_col = by > 0 && bx != 0 && bx + 2 < a.wmb && tid < kGranulesPerMB;
-      const uint64_t* fresh_gp = fresh_col ? gran_at(a, bx + 2, by - 1, tid) : nullptr;
+      if (!kDecode && bx + 1 < ap->wmb) src_dma(*ap, bx + 1, by, L.src[(bx + 1) & 1]);
+      const bool fresh_col = by > 0 && bx != 0 && bx + 2 < ap->wmb && tid < kGranulesPerMB;
+      const uint64_t* fresh_gp = fresh_col ? gran_at(*ap, bx + 2, by - 1, tid) : nullptr;
       const uint64_t fresh_g = fresh_col ? gran_ld(fresh_gp) : 0;
       // At a group start the coder needs the group's inter records, and every
       // cross-frame dependency they carry (the stale rows, references and
@@ -2015,13 +2016,13 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       // already, so their loads go out here, in flight with the fresh
       // granule's, instead of a round trip of their own after it (settled by
       // tag in load_inter).  At a group start, after the search.
-      const int nref = a.inter ? a.ring - 1 : 0;
+      const int nref = ap->inter ? ap->ring - 1 : 0;
       uint64_t rg[kMaxRing - 1][2];
       auto issue_records = [&]() {
 #pragma unroll
         for (int o = 0; o < kMaxRing - 1; o++) {
           if (o >= nref) break;
-          const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
+          const uint64_t* r = (const uint64_t*)&ap->inter_desc[o * mbs + mb];
           rg[o][0] = gran_ld(r);
           rg[o][1] = gran_ld(r + 1);
         }
@@ -2031,7 +2032,7 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       {  // diagnostic (tools builds): how long the previous macroblock's stores still take here
         const uint64_t ts = acct_now();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        acct_add(a.acct, Acct::kCoderStoreTail, acct_now() - ts);
+        acct_add(ap->acct, Acct::kCoderStoreTail, acct_now() - ts);
       }
 #endif
       uint64_t tacc = acct_now();
@@ -2041,21 +2042,21 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       // macroblock's record of reference 1 -- the helper's last search, after
       // its wait for the previous frame -- carries this frame's tag; otherwise
       // (intra and decoded frames: the helper's carrier) once inter_done says so.
-      const bool by_tag = a.inter;  // workgroup-uniform
-      const uint64_t* grec = (const uint64_t*)&a.inter_desc[mb];  // reference 1, this MB
+      const bool by_tag = ap->inter;  // workgroup-uniform
+      const uint64_t* grec = (const uint64_t*)&ap->inter_desc[mb];  // reference 1, this MB
       uint64_t rd0 = 0;
       if (early && tid == 0)
         rd0 = by_tag ? gran_ld(grec)
-                     : (uint64_t)__hip_atomic_load(&a.inter_done[by * a.ng + (bx >> 2)], __ATOMIC_RELAXED,
+                     : (uint64_t)__hip_atomic_load(&ap->inter_done[by * ap->ng + (bx >> 2)], __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       bool ready0 = false;  // thread 0: the records were in before the search
       if (gstart && !early) {  // inter records of MBs bx..bx+3, and every cross-frame dependency they carry
         if (tid == 0) {
-          if (by_tag) rec_settle(a, grec, gran_ld(grec), by, mb);
-          else wait_records(a, by, bx >> 2);
+          if (by_tag) rec_settle(*ap, grec, gran_ld(grec), by, mb);
+          else wait_records(*ap, by, bx >> 2);
         }
-        acquire_after_wait(a.sys);  // the stale rows, references and previous output_cache
-        acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
+        acquire_after_wait(ap->sys);  // the stale rows, references and previous output_cache
+        acct_add(ap->acct, Acct::kCoderGroupWait, acct_now() - tacc);
       }
       tacc = acct_now();
 
@@ -2070,27 +2071,27 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         if (bx == 0) {
           int lx[9], ly[9], n = 0;
           for (int r = max(by - 3, 0); r <= by - 1; r++)
-            for (int c = 0; c <= 2 && c < a.wmb; c++) lx[n] = c, ly[n++] = r;
+            for (int c = 0; c <= 2 && c < ap->wmb; c++) lx[n] = c, ly[n++] = r;
           for (int k = tid; k < n * kGranulesPerMB; k += 256) {
             const int i = k / kGranulesPerMB, kk = k - i * kGranulesPerMB;
-            const uint64_t* gp = gran_at(a, lx[i], ly[i], kk);
-            win_put_k(L.win, oy, lx[i], ly[i], kk, gran_settle(a, gp, gran_ld(gp), by));
+            const uint64_t* gp = gran_at(*ap, lx[i], ly[i], kk);
+            win_put_k(L.win, oy, lx[i], ly[i], kk, gran_settle(*ap, gp, gran_ld(gp), by));
           }
         } else if (fresh_col) {
           win_put_k(L.win, oy, bx + 2, by - 1, tid,
-                    gran_settle(a, fresh_gp, fresh_g, by));
+                    gran_settle(*ap, fresh_gp, fresh_g, by));
         }
       }
-      acct_add(a.acct, Acct::kCoderWindow, acct_now() - tacc);
+      acct_add(ap->acct, Acct::kCoderWindow, acct_now() - tacc);
       // the source DMA has landed (free where the granule wait above covered
       // it): a wait the compiler sees, so it knows no LDS-DMA is in flight and
       // the barrier before the search does not drain the loads issued below
       const uint64_t tv0 = acct_now();
       if (!kDecode) __builtin_amdgcn_s_waitcnt(kWaitVm0);
-      acct_add(a.acct, Acct::kCoderVm0, acct_now() - tv0);
+      acct_add(ap->acct, Acct::kCoderVm0, acct_now() - tv0);
       if (early && tid == 0) {
-        ready0 = by_tag ? (uint32_t)(rd0 >> 32) == a.epoch : (int)rd0 >= a.nref;
-        if (ready0) acquire_fence(a.sys);  // completes during the search; waited for after it
+        ready0 = by_tag ? (uint32_t)(rd0 >> 32) == ap->epoch : (int)rd0 >= ap->nref;
+        if (ready0) acquire_fence(ap->sys);  // completes during the search; waited for after it
       }
       // source rows of this lane's group slot
       SrcRow s;  // biased u16 pairs (the encoder's source; unused when decoding)
@@ -2104,14 +2105,14 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         s.u[0] = m[128 + co] ^ 0x80008000u, s.u[1] = m[128 + co + 1] ^ 0x80008000u;
         s.v[0] = m[160 + co] ^ 0x80008000u, s.v[1] = m[160 + co + 1] ^ 0x80008000u;
       }
-      const bool pf3 = by >= 3 && bx + 3 < a.wmb, pf2 = by >= 2 && bx + 3 < a.wmb;
-      const bool pfs = by + 1 < a.hmb && bx + 1 < a.wmb;
+      const bool pf3 = by >= 3 && bx + 3 < ap->wmb, pf2 = by >= 2 && bx + 3 < ap->wmb;
+      const bool pfs = by + 1 < ap->hmb && bx + 1 < ap->wmb;
       uint64_t pg3 = 0, pg2 = 0;
       uint32_t pst = 0;
       if (tid < kGranulesPerMB) {
-        if (pf3) pg3 = gran_ld(gran_at(a, bx + 3, by - 3, tid));
-        if (pf2) pg2 = gran_ld(gran_at(a, bx + 3, by - 2, tid));
-        if (pfs && !early) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);  // (early: after the wait)
+        if (pf3) pg3 = gran_ld(gran_at(*ap, bx + 3, by - 3, tid));
+        if (pf2) pg2 = gran_ld(gran_at(*ap, bx + 3, by - 2, tid));
+        if (pfs && !early) pst = *(const uint32_t*)win_src(cs, ap->wa, bx, by + 1, tid);  // (early: after the wait)
       }
 
       // ---- inter predictions, prefetched (the K1 records are final) ----
@@ -2121,40 +2122,44 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       // the minimum over the references alone -- known from the records,
       // before the search.  Its block (and a sub-pel winner's neighbour)
       // loads overlap the search.
-      BlockDesc ib;
+      BlockDesc ib;  // set by reference 1 (o == 0) before it is compared
       int ib_sad = 0;
       int ipa[2] = {0, 0}, ipb[2] = {0, 0};
       auto load_inter = [&]() {  // the records (issue_records), then the predictions
 #pragma unroll
         for (int o = 0; o < kMaxRing - 1; o++) {
           if (o >= nref) break;
-          const uint64_t* r = (const uint64_t*)&a.inter_desc[o * mbs + mb];
-          const BlockDesc rd = unpack_inter_desc((uint32_t)uni((int)rec_settle(a, r, rg[o][0], by, mb)));
-          const int rs = uni((int)rec_settle(a, r + 1, rg[o][1], by, mb));
-          const bool ci = (rd.block_type & kCopy) != 0, cb = (ib.block_type & kCopy) != 0;
-          if (o == 0 || (ci != cb ? ci : rs < ib_sad)) ib = rd, ib_sad = rs;
+          const uint64_t* r = (const uint64_t*)&ap->inter_desc[o * mbs + mb];
+          const BlockDesc rd = unpack_inter_desc((uint32_t)uni((int)rec_settle(*ap, r, rg[o][0], by, mb)));
+          const int rs = uni((int)rec_settle(*ap, r + 1, rg[o][1], by, mb));
+          if (o == 0) {
+            ib = rd, ib_sad = rs;
+          } else {
+            const bool ci = (rd.block_type & kCopy) != 0, cb = (ib.block_type & kCopy) != 0;
+            if (ci != cb ? ci : rs < ib_sad) ib = rd, ib_sad = rs;
+          }
         }
         if (nref == 0) return;
         const BlockDesc& d = ib;
-        const PlaneSet rp = RECON_AT(a, d.prediction_target);
+        const PlaneSet rp = RECON_AT(*ap, d.prediction_target);
         const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
         const int mx = px + (mot ? d.motion_x : 0), my = py + (mot ? d.motion_y : 0);
         int dx = 0, dy = 0;
         if (sp) frac_dir(d.sp_index, &dx, &dy);
         _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
-          ipa[bi] = pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, mx, my);
-          if (sp) ipb[bi] = pred_at(rp, a.wa, (wave + 4 * bi) * 64 + lane, mx + dx, my + dy);
+          ipa[bi] = pred_at(rp, ap->wa, (wave + 4 * bi) * 64 + lane, mx, my);
+          if (sp) ipb[bi] = pred_at(rp, ap->wa, (wave + 4 * bi) * 64 + lane, mx + dx, my + dy);
         }
       };
       const uint64_t tr0 = acct_now();
       if (!early) load_inter();
-      stamp(a, mb, 1);
+      stamp(*ap, mb, 1);
       const uint64_t tr1 = acct_now();
       __syncthreads();
-      stamp(a, mb, 2);
+      stamp(*ap, mb, 2);
       tacc = acct_now();
-      acct_add(a.acct, Acct::kCoderRecords, tr1 - tr0);
-      acct_add(a.acct, Acct::kCoderPreBarrier, tacc - tr1);
+      acct_add(ap->acct, Acct::kCoderRecords, tr1 - tr0);
+      acct_add(ap->acct, Acct::kCoderPreBarrier, tacc - tr1);
 
       BlockDesc d;
       bool from_inter = false;  // an inter record won / an inter type is decoded (prediction in wpv)
@@ -2174,15 +2179,17 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         sel.ssd = INT32_MAX;
         sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
         int buf = 0;
+        uint64_t t_ev = 0, t_ba = 0, t_se = 0;  // (CAIRO_ACCT builds: the stages' phases)
   #pragma unroll 1
         for (int stage = 0; stage < ((CAIRO_ATTR_SKIP & 16) ? 0 : 5); stage++) {
           const int step = stage == 0 ? kRadius : (kRadius >> stage);
           const int jlo = stage == 0 ? -2 * kRadius : -step;
           const int bx0 = sel.bx, by0 = sel.by;
+          const uint64_t ts0 = acct_now();
           if (grp < 9) {  // group g < 9 evaluates candidate g; groups 9..15 idle (7/16 of the work saved)
             const int c = min(grp, 8);
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
-            const bool ok = intra_valid(cx, cy, px, py, a.wa, a.ha);
+            const bool ok = intra_valid(cx, cy, px, py, ap->wa, ap->ha);
             int sad, mad;
             cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
             if (gi == 0 && grp < 9) {
@@ -2190,7 +2197,9 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
               L.cand[buf][grp][1] = mad;
             }
           }
+          const uint64_t ts1 = acct_now();
           __syncthreads();
+          const uint64_t ts2 = acct_now();
           {
             const int c = lane & 15;
             const int vs = L.cand[buf][c][0], vm = L.cand[buf][c][1];
@@ -2198,8 +2207,15 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
             select_int(sel, c < 9 && vs >= 0, cx, cy, vs, vm, px, py, thr, lane);
           }
           buf ^= 1;
+          if (CAIRO_ACCT) {
+            const uint64_t ts3 = uni((int)sel.bx) == -99999 ? 0 : acct_now();  // after the replay's result
+            t_ev += ts1 - ts0, t_ba += ts2 - ts1, t_se += ts3 - ts2;
+          }
         }
-        stamp(a, mb, 3);
+        acct_add(ap->acct, Acct::kSrchEval, t_ev);
+        acct_add(ap->acct, Acct::kSrchBarrier, t_ba);
+        acct_add(ap->acct, Acct::kSrchSelect, t_se);
+        stamp(*ap, mb, 3);
         if (!(CAIRO_ATTR_SKIP & 16)) {  // sub-pel (perform_intra_subpixel_motion_search, motion.cpp:277-317)
           const int bx0 = sel.bx, by0 = sel.by;
           // candidate c = 2 nn + q; q is wave-uniform (waves 0 and 2 the half
@@ -2207,37 +2223,46 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           const int q = (grp >> 2) & 1, nn = (grp & 3) | ((grp >> 3) << 2), c = 2 * nn + q;
           const int k9 = nn < 4 ? nn : nn + 1;  // skip the centre of the 3x3
           const int tx = bx0 + k9 % 3 - 1, ty = by0 + k9 / 3 - 1;
-          const bool ok = intra_valid(tx, ty, px, py, a.wa, a.ha);
+          const bool ok = intra_valid(tx, ty, px, py, ap->wa, ap->ha);
           int sad, mad;
+          const uint64_t ts0 = acct_now();
           subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, uni(q), gi, s, sad, mad);
           if (gi == 0) {
             L.cand[buf][c][0] = ok ? sad : -1;
             L.cand[buf][c][1] = mad;
           }
+          const uint64_t ts1 = acct_now();
           __syncthreads();
+          const uint64_t ts2 = acct_now();
           const int vs = L.cand[buf][lane & 15][0], vm = L.cand[buf][lane & 15][1];
           sel.sp_idx = sel.sp_amt = sel.sp_en = 0;
           select_sub(sel, vs >= 0, vs, vm, thr, lane);
+          if (CAIRO_ACCT) {
+            const uint64_t ts3 = uni((int)sel.sp_idx) == -99999 ? 0 : acct_now();
+            acct_add(ap->acct, Acct::kSubEval, ts1 - ts0);
+            acct_add(ap->acct, Acct::kSubBarrier, ts2 - ts1);
+            acct_add(ap->acct, Acct::kSubSelect, ts3 - ts2);
+          }
         }
-        stamp(a, mb, 4);
-        acct_add(a.acct, Acct::kCoderSearch, acct_now() - tacc);
+        stamp(*ap, mb, 4);
+        acct_add(ap->acct, Acct::kCoderSearch, acct_now() - tacc);
         if (early) {  // the group's records (and the cross-frame dependencies), then this MB's
           tacc = acct_now();
           if (tid == 0) {
             if (!ready0) {
-              if (by_tag) rec_settle(a, grec, gran_ld(grec), by, mb);
-              else wait_records(a, by, bx >> 2);
-              acquire_fence(a.sys);
+              if (by_tag) rec_settle(*ap, grec, gran_ld(grec), by, mb);
+              else wait_records(*ap, by, bx >> 2);
+              acquire_fence(ap->sys);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the acquire has completed
           }
           __syncthreads();
-          acct_add(a.acct, Acct::kCoderGroupWait, acct_now() - tacc);
+          acct_add(ap->acct, Acct::kCoderGroupWait, acct_now() - tacc);
           tacc = acct_now();
-          if (tid < kGranulesPerMB && pfs) pst = *(const uint32_t*)win_src(cs, a.wa, bx, by + 1, tid);
+          if (tid < kGranulesPerMB && pfs) pst = *(const uint32_t*)win_src(cs, ap->wa, bx, by + 1, tid);
           issue_records();
           load_inter();
-          acct_add(a.acct, Acct::kCoderInter, acct_now() - tacc);
+          acct_add(ap->acct, Acct::kCoderInter, acct_now() - tacc);
         }
         d = make_desc(sel, px, py, thr, true, 0);
         int best_sad = sel.sad;
@@ -2261,22 +2286,22 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       } else {
         // ---- decoder (decode_slice, decode.cpp:146-170): the block desc is
         //      given; an inter type predicts from its reference slot ----
-        const uint4 tw = *(const uint4*)&a.table[mb];
+        const uint4 tw = *(const uint4*)&ap->table[mb];
         d = uni_desc_words(tw);
         d.q_index = (uint8_t)(uni((int)tw.w) >> 8);  // uni_desc leaves it to the quantizer
         if (!(d.block_type & kIntra)) {
           from_inter = true;
-          const PlaneSet rp = RECON_AT(a, d.prediction_target);
+          const PlaneSet rp = RECON_AT(*ap, d.prediction_target);
           const bool mot = (d.block_type & kMotion) != 0, sp = mot && d.sp_pred;
           int dx = 0, dy = 0;
           if (sp) frac_dir(d.sp_index, &dx, &dy);
           _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
-            wpv[bi] = pred_global(rp, a.wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
+            wpv[bi] = pred_global(rp, ap->wa, (wave + 4 * bi) * 64 + lane, px + (mot ? d.motion_x : 0),
                                   py + (mot ? d.motion_y : 0), sp, dx, dy, d.sp_amount);
         }
       }
       ap = opaque_view(ap);  // after the searches: the view's fields re-read, not live across them
-      stamp(a, mb, 5);
+      stamp(*ap, mb, 5);
       const uint64_t tx5 = acct_now();
       // this lane's source elements for the residual, loaded after the
       // searches: live across them, they pushed the engine into scratch
@@ -2327,7 +2352,7 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           cf[bi] = (CAIRO_ATTR_SKIP & 64) ? res : fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane, res);
         }
       }
-      stamp(a, mb, 6);
+      stamp(*ap, mb, 6);
       // The prefetched window blocks for MB bx+1 (loaded before the search),
       // into the window before this macroblock's first store: settled after
       // the stores, their wait (vmcnt retires in order) also waited for the
@@ -2338,17 +2363,17 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       if (tid < kGranulesPerMB) {
         if (pf3)
           win_put_k(L.win, oy, bx + 3, by - 3, tid,
-                    gran_settle(a, gran_at(a, bx + 3, by - 3, tid), pg3, by));
+                    gran_settle(*ap, gran_at(*ap, bx + 3, by - 3, tid), pg3, by));
         if (pf2)
           win_put_k(L.win, oy, bx + 3, by - 2, tid,
-                    gran_settle(a, gran_at(a, bx + 3, by - 2, tid), pg2, by));
+                    gran_settle(*ap, gran_at(*ap, bx + 3, by - 2, tid), pg2, by));
         if (pfs) win_put_k(L.win, oy, bx, by + 1, tid, pst);
       }
       if (!(type & kCopy)) {
         int qp;
         if (!kDecode) {
           int32_t v2;
-          qp = vaq_mb(L.red, wave, lane, cf[0], a.quality, &v2);
+          qp = vaq_mb(L.red, wave, lane, cf[0], ap->quality, &v2);
           d.q_index = (uint8_t)qp;
           d.variance = (int16_t)v2;
         } else {
@@ -2359,11 +2384,11 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           int16_t qv;
           if (!kDecode) {
             qv = (CAIRO_ATTR_SKIP & 64) ? (int16_t)cf[bi] : quant_elem(e, cf[bi], qp, intra_path);
-            coef_store_pair(a, e, px, py, qv);
+            coef_store_pair(*ap, e, px, py, qv);
           } else {  // the decoded coefficients (the decoder's input_cache)
             int pl, ex, ey;
             elem_coords(e, px, py, pl, ex, ey);
-            qv = plane_of(planes(a.coef), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+            qv = plane_of(planes(ap->coef), pl)[(size_t)ey * (pl ? cw : ap->wa) + ex];
           }
           const int t = (CAIRO_ATTR_SKIP & 64) ? qv
                                                : idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
@@ -2379,13 +2404,13 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
             const int e = (wave + 4 * bi) * 64 + lane;
             int pl, ex, ey;
             elem_coords(e, px, py, pl, ex, ey);
-            cp[bi] = pick(planes(a.coef_prev), pl)[(size_t)ey * (pl ? cw : a.wa) + ex];
+            cp[bi] = pick(planes(ap->coef_prev), pl)[(size_t)ey * (pl ? cw : ap->wa) + ex];
           }
           _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk)
-            coef_store_pair(a, (wave + 4 * bi) * 64 + lane, px, py, cp[bi]);
+            coef_store_pair(*ap, (wave + 4 * bi) * 64 + lane, px, py, cp[bi]);
         }
       }
-      stamp(a, mb, 7);
+      stamp(*ap, mb, 7);
       const uint64_t tx7 = acct_now();
       asm volatile("" ::: "memory");  // program order: the coefficient stores, then (kStoresAfterCoef) ...
       // publish first (the next row's coder waits for exactly these): pixel
@@ -2400,11 +2425,11 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         if (!(lane & 1)) {
           const int r = lane >> 3, c2 = (lane & 7) >> 1;
           const int k = b < 4 ? (((b >> 1) * 8 + r) * 8 + (b & 1) * 4 + c2) : (128 + (b - 4) * 32 + r * 4 + c2);
-          gran_st(gran_at(a, bx, by, k),
+          gran_st(gran_at(*ap, bx, by, k),
                   ((uint64_t)tag << 32) | ((uint32_t)pv[bi] & 0xFFFFu) | ((uint32_t)nb << 16));
         }
       }
-      stamp(a, mb, 8);
+      stamp(*ap, mb, 8);
       // reconstruction -> the window (the slot is written by the deblock,
       // from the granules)
       _Pragma("unroll") for (int bi = 0; bi < 2; bi++) if (bi < nblk) {
@@ -2414,7 +2439,7 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
         win_put1(L.win, pl, pl == 0 ? ey - oy : ey - (oy >> 1), ex, pv[bi]);
       }
       asm volatile("" ::: "memory");  // ... the pixel-granule stores, then the table store
-      if (tid == 0 && !kDecode) *(uint4*)&a.table[mb] = __builtin_bit_cast(uint4, d);  // one 16-byte store
+      if (tid == 0 && !kDecode) *(uint4*)&ap->table[mb] = __builtin_bit_cast(uint4, d);  // one 16-byte store
       // every wave's coefficient stores drained, then the block info for the
       // deblock (its edge strengths); thread 0's drain covers only wave 0, so
       // the other waves drain before the barrier of the next macroblock --
@@ -2435,17 +2460,16 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
       }
       __syncthreads();
       if (tid == 0)
-        gran_st(gran_at(a, bx, by, kGranulesPerMB),
+        gran_st(gran_at(*ap, bx, by, kGranulesPerMB),
                 ((uint64_t)tag << 32) | ((d.block_type & kCopy) ? 0x100u : 0u) | d.q_index);
-      stamp(a, mb, 9);
+      stamp(*ap, mb, 9);
       if (CAIRO_ACCT) {
         const uint64_t tx9 = acct_now();
-        acct_add(a.acct, Acct::kCoderXform, tx7 - tx5);
-        acct_add(a.acct, Acct::kCoderPublish, tx8 - tx7);
-        acct_add(a.acct, Acct::kCoderDrain, tx9 - tx8);
+        acct_add(ap->acct, Acct::kCoderXform, tx7 - tx5);
+        acct_add(ap->acct, Acct::kCoderPublish, tx8 - tx7);
+        acct_add(ap->acct, Acct::kCoderDrain, tx9 - tx8);
       }
-      if (a.stamps && tid == 0) a.stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
-#undef a
+      if (ap->stamps && tid == 0) ap->stamps[(size_t)mb * kStampPhases + 11] = __builtin_amdgcn_s_memtime();
     }
   }
 }

@@ -62,6 +62,10 @@ def main():
     coder = {k: round(us(c["coder_" + k]) / mbs, 3) for k in ("total",) + parts}
     coder["rest"] = round(coder["total"] - sum(coder[k] for k in parts), 3)
     coder["dequeue_per_task"] = round(us(c["coder_dequeue"]) / max(c["coder_tasks"], 1), 2)
+    # inside "search": thread 0's wave per stage phase (evaluation + LDS stores, barrier, LDS reads + replay)
+    coder["search_phases"] = {k: round(us(c[k]) / mbs, 3) for k in
+                              ("search_eval", "search_barrier", "search_select", "subpel_eval", "subpel_barrier",
+                               "subpel_select")}
     helper = {k: round(us(c["helper_" + k]) / groups, 3) for k in ("total", "wait", "deblock", "search", "catchup")}
     helper["rest"] = round(helper["total"] - sum(helper[k] for k in ("wait", "deblock", "search", "catchup")), 3)
     helper["dequeue_per_task"] = round(us(c["helper_dequeue"]) / max(c["helper_tasks"], 1), 2)

@@ -8,10 +8,14 @@ Per quality q, on the band4 content (seed 1234), ring R = 4:
     entropy), plus the 10-byte frame descriptor the encoder writes per frame;
   * distortion: PSNR (peak 255) of the last frame's deblocked reconstruction
     against its converted source, luma and chroma separately.
-  * a pin: the canonical SHA-256 (tail bits and header byte 7 masked) of the
-    stream records of frames 0..--check-1 as the pipeline produced them, so
-    that tests/test_rd_sweep_pinned.py can compare the committed table with the
-    oracle on the CPU (this tool itself never loads the oracle).
+  * parity: the canonical FNV-1a-64 (tail bits and header byte 7 masked) of
+    every frame's stream record that the oracle's golden stream of this quality
+    covers (tests/golden/stream_4k_q<q>_r4.json, made off-box by
+    tests/golden/make_stream_golden.py: 40 frames, all three references live
+    from frame 3) is compared here, and the hashes are kept in the row, so that
+    tests/test_rd_sweep_pinned.py ties the committed table to the goldens and
+    the goldens to the oracle (this tool uses the oracle library only for its
+    FNV-1a-64, never its encoder).
 Writes one JSON object per q to stdout and the whole table to --out.
 usage (GPU box): python tools/rd_sweep.py [--config 4k] [--frames 48] [--q 1,4,8,...]
 """
@@ -36,28 +40,26 @@ def psnr(a, b):
     return float("inf") if mse == 0 else 10.0 * math.log10(255.0 ** 2 / mse)
 
 
-def record_sha(w, h, ring, q, t, payload, nbits):
-    """Canonical SHA-256 (16 hex digits) of frame t's stream record: header or
-    descriptor + payload, bits beyond the end and header byte 7 zeroed."""
+def record_hashes(w, h, ring, q, t, payload, nbits):
+    """Canonical SHA-256 (16 hex digits) and FNV-1a-64 of frame t's stream
+    record: header or descriptor + payload, bits beyond the end and header
+    byte 7 zeroed (oracle.canonical_frame_bytes), and its bit count."""
     import cairo_amd
+    from oracle import oracle as orc
 
     rec, n = bench.record(cairo_amd, w, h, ring, q, t, payload, nbits)
-    b = bytearray(rec[: (n + 7) // 8])
-    if n % 8:
-        b[-1] &= (1 << (n % 8)) - 1
-    if t == 0 and len(b) > 7:
-        b[7] = 0
-    return hashlib.sha256(bytes(b)).hexdigest()[:16], n
+    b = orc.canonical_frame_bytes(rec, n, t == 0)
+    return hashlib.sha256(b).hexdigest()[:16], f"{orc.fnv1a64(b):016x}", n
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="4k", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=160, help="timed P-frames per quality")
-    ap.add_argument("--q", default="1,2,4,8,12,16,20,24,28,31")
+    ap.add_argument("--q", default=",".join(str(q) for q in range(1, 32)))
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rd_sweep.json"))
     ap.add_argument("--check", type=int, default=8,
-                    help="frames per quality pinned by their record hashes (SURVEY §8(d) Config 5: >= 8)")
+                    help="frames per quality also pinned by SHA-256 (SURVEY §8(d) Config 5: >= 8)")
     a = ap.parse_args()
     import torch
 
@@ -95,14 +97,20 @@ def main():
         tks = []
         bits = []
         pins = []
+        gold = bench.golden_stream(a.config, "band4", q, ring)
+        ncheck = min(n, gold["frames"]) if gold else 0
+        fnv = []
 
         def take(tk):
             data, nb = st.collect(tk)
             t = len(bits)
             bits.append(nb)
-            if t < a.check:
-                sha, rec_bits = record_sha(w, h, ring, q, t, data, nb)
-                pins.append({"frame": t, "record_bits": rec_bits, "sha256_16": sha})
+            if t < max(a.check, ncheck):
+                sha, h64, rec_bits = record_hashes(w, h, ring, q, t, data, nb)
+                if t < a.check:
+                    pins.append({"frame": t, "record_bits": rec_bits, "sha256_16": sha})
+                if t < ncheck:
+                    fnv.append(h64)
 
         for f in range(n):
             tks.append(st.submit(ptr(f), f, f > 0, q, on_device=True))
@@ -125,6 +133,9 @@ def main():
                "psnr_u": round(psnr(src[1][:hh // 2, :ww // 2], rec[1][:hh // 2, :ww // 2]), 2),
                "psnr_v": round(psnr(src[2][:hh // 2, :ww // 2], rec[2][:hh // 2, :ww // 2]), 2),
                "pinned_frames": pins}
+        mism = [t for t in range(ncheck) if fnv[t] != gold["frame_fnv1a64"][t]]
+        row["golden"] = {"path": gold["path"] if gold else None, "frames_checked": ncheck,
+                         "mismatches": len(mism), "mismatched_frames": mism, "frame_fnv1a64": fnv}
         rows.append(row)
         print(json.dumps(row), flush=True)
     out = {"config": f"{w}x{h} p-frames, ring R={ring}, band4 seed 1234 (BASELINE.json configs[4])",
