@@ -141,6 +141,52 @@ __global__ void __launch_bounds__(256) k_hop(Args a) {
   }
 }
 
+// Stale-line probe (mode "stale"): can a workgroup on one XCD, after an
+// agent-scope acquire that observed a producer's flag, still read a line its
+// XCD's L2 cached before the producer (on another XCD) wrote it?  Per trial k
+// on its own 128-byte line: the consumer loads the line (plain) and raises
+// `loaded`; the producer, seeing it, stores the line's word -- sc1 (write-
+// through, as the engine's coefficient stores) or plain followed by a release
+// fence -- drains and raises `written` (release); the consumer acquires and
+// reloads the word plainly and with an sc1 load.  Counts of stale values.
+__global__ void __launch_bounds__(64) k_stale(uint32_t* data, uint32_t* flags, uint32_t* out, int trials,
+                                              int plain_store) {
+  const bool producer = blockIdx.x == 0, consumer = blockIdx.x == 1;
+  if (!(producer || consumer) || threadIdx.x != 0) return;
+  uint32_t stale_plain = 0, stale_sc1 = 0, timeouts = 0, sink = 0;
+  for (int k = 0; k < trials; k++) {
+    uint32_t* word = data + (size_t)k * 32;  // one line per trial
+    const uint32_t v = 0x5A000000u | (uint32_t)k;
+    if (consumer) {
+      sink += *(volatile uint32_t*)word;  // the line into this XCD's L1/L2 (value 0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(flags + 0, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(flags + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)(k + 1))
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kLimit) { timeouts++; k = trials; break; }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const uint32_t a = *(volatile uint32_t*)word;
+      const uint32_t b = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      stale_plain += a != v;
+      stale_sc1 += b != v;
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(flags + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)(k + 1))
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kLimit) { timeouts++; k = trials; break; }
+      if (plain_store) {
+        *(volatile uint32_t*)word = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      } else {
+        __hip_atomic_store(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(flags + 32, (uint32_t)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (consumer) out[0] = stale_plain, out[1] = stale_sc1, out[2] = sink, out[4] = timeouts;
+  else out[3] = timeouts;
+}
+
 static size_t buf_bytes(int pay_words) { return (size_t)(kPay + 2 * pay_words + 64) * 4; }
 
 static void report(const char* what, const uint32_t* t, int iters, int pay_bytes) {
@@ -187,6 +233,25 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(t.data(), a.times, (iters + 1) * 4, hipMemcpyDeviceToHost));
     const std::string what = std::string("local-") + argv[2] + "-" + argv[3] + "-xcd";
     report(what.c_str(), t.data(), iters, pay * 4);
+    return 0;
+  }
+  if (mode == "stale" && argc == 4) {  // stale <sc1|plain> <trials>
+    const int plain = std::string(argv[2]) == "plain", trials = atoi(argv[3]);
+    uint32_t *data, *flags, *out;
+    CK(hipMalloc(&data, (size_t)trials * 128));
+    CK(hipMemset(data, 0, (size_t)trials * 128));
+    CK(hipMalloc(&flags, 256));
+    CK(hipMemset(flags, 0, 256));
+    CK(hipMalloc(&out, 64));
+    CK(hipMemset(out, 0, 64));
+    hipLaunchKernelGGL(k_stale, dim3(2), dim3(64), 0, 0, data, flags, out, trials, plain);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    uint32_t o[5];
+    CK(hipMemcpy(o, out, sizeof(o), hipMemcpyDeviceToHost));
+    printf("{\"mode\": \"stale-%s-store\", \"trials\": %d, \"stale_plain_loads\": %u, \"stale_sc1_loads\": %u, "
+           "\"timeouts\": %u}\n",
+           plain ? "plain+release" : "sc1", trials, o[0], o[1], o[3] + o[4]);
     return 0;
   }
   if ((mode == "ping" || mode == "pong") && argc == 5) {

@@ -57,10 +57,14 @@ def main():
                 print(json.dumps(rows[-1]), flush=True)
         rows.append(pair(pay, a.iters))
         print(json.dumps(rows[-1]), flush=True)
+    stale = [run(["stale", kind, "4096"]) for kind in ("sc1", "plain")]
+    for r in stale:
+        print(json.dumps(r), flush=True)
     doc = {"what": "one progress-word hop (producer: payload stores, vmcnt(0), barrier, release fence, word; "
                    "consumer: poll, acquire fence, payload loads), ping-pong between two 256-thread workgroups, "
                    "round trip / 2, s_memrealtime; one MI355X (no xGMI link in the path)",
-           "iters": a.iters, "rows": rows}
+           "iters": a.iters, "rows": rows,
+           "stale_line_probe": stale}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(doc, open(a.out, "w"), indent=1)
 
