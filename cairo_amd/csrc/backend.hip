@@ -1194,6 +1194,11 @@ static int frame_result(cairo_ctx* c, Stage& s, cairo_frame_result* out, bool po
     out->feed = (const uint32_t*)h + kFeedHdrWords;
     out->feed_bits = (uint64_t)h[0] | ((uint64_t)h[1] << 32);
     out->feed_status = h[2] ? CAIRO_FEED_OVERFLOW : CAIRO_FEED_VALID;
+    if (!h[2] && h[3]) {  // k_feed_write's bounds guard dropped writes: the feed is not the frame's
+      fprintf(stderr, "[cairo_amd] frame %u: the precode writer found %u writes outside the frame's feed\n",
+              s.index, (uint32_t)h[3]);
+      return kHardwareFail;
+    }
   }
   out->wa = c->wa;
   out->ha = c->ha;

@@ -424,6 +424,17 @@ __device__ __forceinline__ void pk_diff(uint32_t a, uint32_t b, uint32_t& sad, u
   m2 = __builtin_elementwise_max(m2, __builtin_elementwise_sub_sat(as_u16x2(b), as_u16x2(a)));
 }
 
+// The acceptance rules (evaluate_motion_candidate / _subpel_, motion.cpp:111-223)
+// use a candidate's MAD only through "mad < thr" and, in copy mode (the best's
+// MAD below thr), "mad < best mad" / "==": every MAD at or above thr acts the
+// same.  MAD >= max |dY| >= SAD / 256, so a candidate whose luma SAD exceeds
+// 256 * (thr - 1) has MAD >= thr: its exact MAD is never needed, and kMadFar
+// stands for it.  A wave computes the MADs of its candidates only when one of
+// them could be below thr (the search's copy-mode tests, the state's MAD and
+// the block type see the same outcomes).
+constexpr int kMadFar = 65535;
+__device__ __forceinline__ bool mad_needed(int sad, int thr) { return sad <= 256 * (thr - 1); }
+
 // ---------------------------------------------------------------------------
 // Inter-search window in LDS, shared by the 4 waves of a workgroup that search
 // 4 horizontally adjacent macroblocks: 80 luma rows x 128 columns (origin 32 px
@@ -611,33 +622,34 @@ __device__ __forceinline__ uint32_t absdiff_b(uint32_t x, uint32_t y) {  // bias
 // source rows are biased u16 pairs; unaligned columns are realigned with
 // v_alignbyte_b32.  Returns the candidate's SAD (luma) and MAD (luma + chroma)
 // in every lane of the group (compute_block_sad / _mad, analysis.h:42-125).
-__device__ __forceinline__ void inter_cand_row(const Window& w, int wx, int wy, int i, const SrcRow& s,
+__device__ __forceinline__ void inter_cand_row(const Window& w, int wx, int wy, int i, const SrcRow& s, int thr,
                                                int& sad, int& mad) {
+  const int sh = (wx & 1) * 2;
+  const uint32_t* row = (const uint32_t*)&w.y[(wy + i) * kWinLP] + (wx >> 1);
+  uint32_t d[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) d[k] = row[k];
   uint32_t sm = 0;
-  u16x2 m1 = {0, 0}, m2 = {0, 0};
-  {
-    const int sh = (wx & 1) * 2;
-    const uint32_t* row = (const uint32_t*)&w.y[(wy + i) * kWinLP] + (wx >> 1);
-    uint32_t d[9];
 #pragma unroll
-    for (int k = 0; k < 9; k++) d[k] = row[k];
+  for (int k = 0; k < 8; k++) sm = __builtin_amdgcn_sad_u16(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), sm);
+  sad = row16_sum((int)sm);
+  mad = kMadFar;
+  if (__ballot(mad_needed(sad, thr))) {  // (wave-uniform) some candidate of the wave may have MAD < thr
+    u16x2 m1 = {0, 0}, m2 = {0, 0};
+    uint32_t dummy = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) pk_diff(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), sm, m1, m2);
-  }
-  {
-    const int cr = (wy >> 1) + (i >> 1), cc = (wx >> 1) + (i & 1) * 4, sh = (cc & 1) * 2;
+    for (int k = 0; k < 8; k++) pk_diff(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), dummy, m1, m2);
+    const int cr = (wy >> 1) + (i >> 1), cc = (wx >> 1) + (i & 1) * 4, shc = (cc & 1) * 2;
     const uint32_t* ru = (const uint32_t*)&w.u[cr * kWinCP] + (cc >> 1);
     const uint32_t* rv = (const uint32_t*)&w.v[cr * kWinCP] + (cc >> 1);
     const uint32_t u0 = ru[0], u1 = ru[1], u2 = ru[2], v0 = rv[0], v1 = rv[1], v2 = rv[2];
-    uint32_t dummy = 0;
-    pk_diff(s.u[0], __builtin_amdgcn_alignbyte(u1, u0, sh), dummy, m1, m2);
-    pk_diff(s.u[1], __builtin_amdgcn_alignbyte(u2, u1, sh), dummy, m1, m2);
-    pk_diff(s.v[0], __builtin_amdgcn_alignbyte(v1, v0, sh), dummy, m1, m2);
-    pk_diff(s.v[1], __builtin_amdgcn_alignbyte(v2, v1, sh), dummy, m1, m2);
+    pk_diff(s.u[0], __builtin_amdgcn_alignbyte(u1, u0, shc), dummy, m1, m2);
+    pk_diff(s.u[1], __builtin_amdgcn_alignbyte(u2, u1, shc), dummy, m1, m2);
+    pk_diff(s.v[0], __builtin_amdgcn_alignbyte(v1, v0, shc), dummy, m1, m2);
+    pk_diff(s.v[1], __builtin_amdgcn_alignbyte(v2, v1, shc), dummy, m1, m2);
+    const u16x2 m = __builtin_elementwise_max(m1, m2);
+    mad = row16_max(max((int)m.x, (int)m.y));
   }
-  const u16x2 m = __builtin_elementwise_max(m1, m2);
-  sad = row16_sum((int)sm);
-  mad = row16_max(max((int)m.x, (int)m.y));
 }
 
 // Biased source rows of macroblock (px, py) for lane group slot i (SrcRow layout).
@@ -1121,7 +1133,7 @@ __device__ __forceinline__ void inter_task(FA& a0, int r, int g, int off, InterL
           const int cx = bx + (c % 3 - 1) * step, cy = by + (c / 3 - 1) * step;
           const bool ok = in_frame(cx, cy, a.wa, a.ha);
           int sad, mad;
-          inter_cand_row(L.win, (ok ? cx : bx) - ox, (ok ? cy : by) - oy, gi, srow, sad, mad);
+          inter_cand_row(L.win, (ok ? cx : bx) - ox, (ok ? cy : by) - oy, gi, srow, thr, sad, mad);
           const int from = (16 * (my_grp & 3)) << 2;
           const int vs = __builtin_amdgcn_ds_bpermute(from, sad), vm = __builtin_amdgcn_ds_bpermute(from, mad);
           if (my_pass == pass && gi != 4) sadv = vs, madv = vm;
@@ -1796,32 +1808,33 @@ __device__ __forceinline__ void win_put_k(RowWindow& w, int oy, int mbx, int mby
 }
 
 __device__ __forceinline__ void cand_row(const RowWindow& w, int oy, int cx, int cy, int i,
-                                         const SrcRow& s, int& sad, int& mad) {
+                                         const SrcRow& s, int thr, int& sad, int& mad) {
+  const int c = cx & 127, sh = (c & 1) * 2;
+  const uint32_t* row = (const uint32_t*)&w.y[(cy + i - oy) * kCwLP] + (c >> 1);
+  uint32_t d[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) d[k] = row[k];
   uint32_t sm = 0;
-  u16x2 m1 = {0, 0}, m2 = {0, 0};
-  {
-    const int c = cx & 127, sh = (c & 1) * 2;
-    const uint32_t* row = (const uint32_t*)&w.y[(cy + i - oy) * kCwLP] + (c >> 1);
-    uint32_t d[9];
 #pragma unroll
-    for (int k = 0; k < 9; k++) d[k] = row[k];
+  for (int k = 0; k < 8; k++) sm = __builtin_amdgcn_sad_u16(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), sm);
+  sad = row16_sum((int)sm);
+  mad = kMadFar;
+  if (__ballot(mad_needed(sad, thr))) {  // (wave-uniform) some candidate of the wave may have MAD < thr
+    u16x2 m1 = {0, 0}, m2 = {0, 0};
+    uint32_t dummy = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) pk_diff(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), sm, m1, m2);
-  }
-  {
-    const int cr = (cy >> 1) + (i >> 1) - (oy >> 1), cc = ((cx >> 1) + (i & 1) * 4) & 63, sh = (cc & 1) * 2;
+    for (int k = 0; k < 8; k++) pk_diff(s.y[k], __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh), dummy, m1, m2);
+    const int cr = (cy >> 1) + (i >> 1) - (oy >> 1), cc = ((cx >> 1) + (i & 1) * 4) & 63, shc = (cc & 1) * 2;
     const uint32_t* ru = (const uint32_t*)&w.u[cr * kCwCP] + (cc >> 1);
     const uint32_t* rv = (const uint32_t*)&w.v[cr * kCwCP] + (cc >> 1);
     const uint32_t u0 = ru[0], u1 = ru[1], u2 = ru[2], v0 = rv[0], v1 = rv[1], v2 = rv[2];
-    uint32_t dummy = 0;
-    pk_diff(s.u[0], __builtin_amdgcn_alignbyte(u1, u0, sh), dummy, m1, m2);
-    pk_diff(s.u[1], __builtin_amdgcn_alignbyte(u2, u1, sh), dummy, m1, m2);
-    pk_diff(s.v[0], __builtin_amdgcn_alignbyte(v1, v0, sh), dummy, m1, m2);
-    pk_diff(s.v[1], __builtin_amdgcn_alignbyte(v2, v1, sh), dummy, m1, m2);
+    pk_diff(s.u[0], __builtin_amdgcn_alignbyte(u1, u0, shc), dummy, m1, m2);
+    pk_diff(s.u[1], __builtin_amdgcn_alignbyte(u2, u1, shc), dummy, m1, m2);
+    pk_diff(s.v[0], __builtin_amdgcn_alignbyte(v1, v0, shc), dummy, m1, m2);
+    pk_diff(s.v[1], __builtin_amdgcn_alignbyte(v2, v1, shc), dummy, m1, m2);
+    const u16x2 m = __builtin_elementwise_max(m1, m2);
+    mad = row16_max(max((int)m.x, (int)m.y));
   }
-  const u16x2 m = __builtin_elementwise_max(m1, m2);
-  sad = row16_sum((int)sm);
-  mad = row16_max(max((int)m.x, (int)m.y));
 }
 
 // lerp_px on both halves of two biased u16 pairs; the result as a biased pair.
@@ -1838,10 +1851,10 @@ __device__ __forceinline__ uint32_t lerp_pair(uint32_t pa, uint32_t pb, int q) {
 // duplicated tail, realigned by v_alignbyte_b32); the lerped pairs are
 // re-biased so that SAD and MAD use the same packed u16 ops.
 __device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, int by, int tx,
-                                           int ty, int q, int i, const SrcRow& s, int& sad,
+                                           int ty, int q, int i, const SrcRow& s, int thr, int& sad,
                                            int& mad) {
   uint32_t sm = 0;
-  u16x2 m1 = {0, 0}, m2 = {0, 0};
+  uint32_t l[8];  // the lerped luma pairs (biased)
   {
     const int ca = bx & 127, cb = tx & 127, sha = (ca & 1) * 2, shb = (cb & 1) * 2;
     const uint32_t* ra = (const uint32_t*)&w.y[(by + i - oy) * kCwLP] + (ca >> 1);
@@ -1850,11 +1863,20 @@ __device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, i
 #pragma unroll
     for (int k = 0; k < 9; k++) da[k] = ra[k], db[k] = rb[k];
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-      pk_diff(s.y[k],
-              lerp_pair(__builtin_amdgcn_alignbyte(da[k + 1], da[k], sha),
-                        __builtin_amdgcn_alignbyte(db[k + 1], db[k], shb), q),
-              sm, m1, m2);
+    for (int k = 0; k < 8; k++) {
+      l[k] = lerp_pair(__builtin_amdgcn_alignbyte(da[k + 1], da[k], sha),
+                       __builtin_amdgcn_alignbyte(db[k + 1], db[k], shb), q);
+      sm = __builtin_amdgcn_sad_u16(s.y[k], l[k], sm);
+    }
+  }
+  sad = row16_sum((int)sm);
+  mad = kMadFar;
+  if (!__ballot(mad_needed(sad, thr))) return;  // (wave-uniform) kMadFar above
+  u16x2 m1 = {0, 0}, m2 = {0, 0};
+  {
+    uint32_t dummy = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) pk_diff(s.y[k], l[k], dummy, m1, m2);
   }
   {
     const int ra = (by >> 1) + (i >> 1) - (oy >> 1), rb = (ty >> 1) + (i >> 1) - (oy >> 1);
@@ -1875,7 +1897,6 @@ __device__ __forceinline__ void subpel_row(const RowWindow& w, int oy, int bx, i
     }
   }
   const u16x2 m = __builtin_elementwise_max(m1, m2);
-  sad = row16_sum((int)sm);
   mad = row16_max(max((int)m.x, (int)m.y));
 }
 
@@ -2191,7 +2212,7 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
             const int cx = bx0 - step + (c % 3) * step, cy = by0 + jlo + (c / 3) * step;
             const bool ok = intra_valid(cx, cy, px, py, ap->wa, ap->ha);
             int sad, mad;
-            cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, sad, mad);
+            cand_row(L.win, oy, cx, ok ? cy : py - 48, gi, s, thr, sad, mad);
             if (gi == 0 && grp < 9) {
               L.cand[buf][grp][0] = ok ? sad : -1;
               L.cand[buf][grp][1] = mad;
@@ -2226,7 +2247,7 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           const bool ok = intra_valid(tx, ty, px, py, ap->wa, ap->ha);
           int sad, mad;
           const uint64_t ts0 = acct_now();
-          subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, uni(q), gi, s, sad, mad);
+          subpel_row(L.win, oy, bx0, ok ? by0 : py - 48, tx, ok ? ty : py - 48, uni(q), gi, s, thr, sad, mad);
           if (gi == 0) {
             L.cand[buf][c][0] = ok ? sad : -1;
             L.cand[buf][c][1] = mad;

@@ -394,7 +394,7 @@ __global__ __launch_bounds__(64) void k_feed_carry(FeedArgs f) {
   const bool sec_over = lane >= kSecY && lane < kLists && run > kFeedCapacityBits;
   const bool o = __ballot(sec_over) != 0 || all + 64 > (uint64_t)f.feed_stride * 32;
   if (lane < kLists) hdr[4 + lane] = (uint32_t)base;
-  if (lane == 0) hdr[0] = (uint32_t)all, hdr[1] = (uint32_t)(all >> 32), hdr[2] = o ? 1u : 0u;
+  if (lane == 0) hdr[0] = (uint32_t)all, hdr[1] = (uint32_t)(all >> 32), hdr[2] = o ? 1u : 0u, hdr[3] = 0u;
 }
 
 // Per chunk: the table items' codes and positions within their lists, and
@@ -506,9 +506,19 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
   const uint32_t* tpos = tcode + 8 * (size_t)mbs;
   const uint32_t* boff = tpos + 8 * (size_t)mbs;
   uint32_t* feed = f.feed + (size_t)slot * f.feed_stride;
+  // Bounds guard: every word written lies below the frame's feed end (the
+  // words k_feed_scan zeroed, inside the slot's buffer).  A write past it
+  // would be a precode bug: it is dropped and counted in hdr[3], which the
+  // host reports as a hardware failure of the frame (backend.hip
+  // frame_result) instead of coding wrong bits.
+  const uint64_t all_bits = (uint64_t)hdr[0] | ((uint64_t)hdr[1] << 32);
+  const uint64_t limit = min((uint64_t)f.feed_stride, (all_bits + 31) / 32 + 1);
+  uint32_t* const bad = const_cast<uint32_t*>(hdr) + 3;
   if (lane < kTabLists) {
     const uint32_t p = tpos[(size_t)lane * mbs + mb];
-    or_bits(feed, (uint64_t)hdr[4 + lane] + (p & 0x3FFFFFFu), tcode[(size_t)lane * mbs + mb], p >> 26);
+    const uint64_t at = (uint64_t)hdr[4 + lane] + (p & 0x3FFFFFFu);
+    if (((at + (p >> 26) + 31) >> 5) > limit) atomicAdd(bad, 1u);
+    else or_bits(feed, at, tcode[(size_t)lane * mbs + mb], p >> 26);
   }
   if (a.table[mb].block_type & kCopy) return;
   // A block's codes are assembled in LDS words, then stored: the words inside
@@ -537,6 +547,10 @@ __global__ __launch_bounds__(256) void k_feed_write(FeedArgs f) {
     const uint64_t end = pos + ul + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     const uint64_t w0 = pos >> 5;
     const int nw = (int)(((end + 31) >> 5) - w0);  // <= kBlockWords
+    if (w0 + nw > limit || nw > kBlockWords) {  // (wave-uniform) the guard above
+      if (lane == 0) atomicAdd(bad, 1u);
+      return;
+    }
     for (int i = lane; i < nw; i += 64) sw[i] = 0;
     __builtin_amdgcn_wave_barrier();
     const uint32_t rel = (uint32_t)(pos & 31);

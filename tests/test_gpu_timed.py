@@ -67,6 +67,63 @@ def test_timed_4k_many_launches(orc, cairo):
     _run_batched(orc, cairo, 3840, 2160, 4, 16, 44, 10, outputs=cairo.OUT_FEED, device_frames=True)
 
 
+def test_carry_chain_4k_many_launches(cairo):
+    """The round-5 red run's configuration (test_timed_4k_many_launches: 4K
+    q=16 R=4, device frames, feed outputs, 10 frames per launch, 44 frames),
+    repeated in one process with no oracle time: every copy macroblock's
+    coefficients must equal the previous frame's at the same place (the
+    output_cache carry, encode.cpp:69-163 leaves them untouched), the
+    previous frame's plane itself being pinned through the golden stream
+    (every frame's payload hash, whose DC prediction reads copy neighbours'
+    carried coefficients, serialize.cpp:58-72).  DESIGN §2."""
+    import ctypes
+
+    import bench
+    from oracle import oracle as orc
+
+    w, h, ring, q = 3840, 2160, 4, 16
+    frames, batch, iters = 44, 10, 3
+    g = bench.golden_stream("4k", "band4", q, ring)
+    wmb, hmb = w // 16, (h + 15) // 16
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    size = w * h * 3
+    dev = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(frames * size)) == 0
+    try:
+        for t in range(frames):
+            f = cairo.make_band4(w, h, t)
+            assert hip.hipMemcpy(ctypes.c_void_p(dev.value + t * size), f.ctypes.data_as(ctypes.c_void_p),
+                                 ctypes.c_size_t(size), 1) == 0
+        for it in range(iters):
+            ctx = cairo.Context(w, h, ring)
+            ctx.set_outputs(cairo.OUT_FEED)
+            ctx.set_batch(batch)
+            tks = [ctx.submit(dev.value + t * size, t, t > 0, q, on_device=True) for t in range(frames)]
+            prev = None
+            for t, tk in enumerate(tks):
+                out = ctx.wait(tk)
+                data, nb = bench.record(cairo, w, h, ring, q, t, *bench.payload(cairo, ctx, out, tk))
+                got = f"{orc.fnv1a64(orc.canonical_frame_bytes(data, nb, t == 0)):016x}"
+                assert got == g["frame_fnv1a64"][t], f"iteration {it} frame {t}: record differs from the golden"
+                cy, cu, cv = (np.array(p, copy=True) for p in ctx.fetch_coef(tk))
+                if prev is not None:
+                    copy = ((out.table["block_type"] & 4) != 0).reshape(hmb, wmb)
+                    diff = (cy[: hmb * 16].reshape(hmb, 16, wmb, 16) !=
+                            prev[0][: hmb * 16].reshape(hmb, 16, wmb, 16)).any(axis=(1, 3))
+                    for cp, pp in ((cu, prev[1]), (cv, prev[2])):
+                        diff |= (cp[: hmb * 8].reshape(hmb, 8, wmb, 8) !=
+                                 pp[: hmb * 8].reshape(hmb, 8, wmb, 8)).any(axis=(1, 3))
+                    bad = np.argwhere(copy & diff)
+                    assert bad.size == 0, \
+                        f"iteration {it} frame {t}: copy MBs (row, col) {bad[:8].tolist()} lost the previous coefficients"
+                prev = (cy, cu, cv)
+                ctx.release(tk)
+            ctx.sync()
+            ctx.close()
+    finally:
+        hip.hipFree(dev)
+
+
 def _golden_stream_run(cairo, config, frames, batch=0, content="band4"):
     """bench.py's timed leg exactly (its run_hot_path, FrameStore and record
     hashing): `frames` frames of `content` (bench.content_frame) resident in HBM, the library's default
