@@ -282,7 +282,7 @@ class Context:
                    "win_stages", "searched_tasks", "inter_tasks", "coder_xform", "coder_publish", "coder_drain",
                    "coder_vm0", "coder_records", "coder_prebarrier", "coder_store_tail",
                    "search_eval", "search_barrier", "search_select", "subpel_eval", "subpel_barrier",
-                   "subpel_select")
+                   "subpel_select", "db_inputs", "db_filter", "db_write")
 
     def read_acct(self, reset: bool = False) -> dict:
         """Engine time accounting (set_debug(32) on a CAIRO_ACCT=1 build): 10 ns

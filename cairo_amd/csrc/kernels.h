@@ -136,6 +136,10 @@ struct Acct {
   // stores to LDS, the barrier, the LDS reads and the ordered replay
   static constexpr int kSrchEval = 31, kSrchBarrier = 32, kSrchSelect = 33, kSubEval = 34, kSubBarrier = 35,
                        kSubSelect = 36;
+  // inside the helper's deblock chunk: inputs (granules, block info, the rows
+  // above; to the first barrier), the filters, the write-out (stores, drain,
+  // progress word)
+  static constexpr int kDbInputs = 37, kDbFilter = 38, kDbWrite = 39;
 };
 
 // Frames per engine launch.

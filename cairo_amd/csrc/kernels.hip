@@ -2370,7 +2370,10 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
           elem_coords(e, px, py, pl, ex, ey);
           const int sv = svp[bi];
           const int16_t res = has_pred ? (int16_t)(sv - pv[bi]) : (int16_t)sv;
-          cf[bi] = (CAIRO_ATTR_SKIP & 64) ? res : fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane, res);
+          // a zero block transforms to zero (transform.cpp:264-301: every term
+          // and every rounded_div of 0 is 0): no LDS passes (wave-uniform)
+          cf[bi] = (CAIRO_ATTR_SKIP & 64) ? res
+                   : (__ballot(res != 0) ? fdct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane, res) : 0);
         }
       }
       stamp(*ap, mb, 6);
@@ -2411,9 +2414,13 @@ __device__ __forceinline__ void code_row(FA& a0, int by, RowLds& L, int* flag, i
             elem_coords(e, px, py, pl, ex, ey);
             qv = plane_of(planes(ap->coef), pl)[(size_t)ey * (pl ? cw : ap->wa) + ex];
           }
+          // a block whose coefficients all quantized to zero inverse-transforms
+          // to zero (transform.cpp:330-366, per-term truncations of 0): its
+          // reconstruction is the prediction, without the LDS passes
           const int t = (CAIRO_ATTR_SKIP & 64) ? qv
-                                               : idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
-                                                           dequant_elem(e, qv, qp, intra_path));
+                        : (__ballot(qv != 0) ? idct_lane(&L.bufA[b * 64], &L.bufB[b * 64], lane,
+                                                         dequant_elem(e, qv, qp, intra_path))
+                                             : 0);
           pv[bi] = (int16_t)(has_pred ? t + pv[bi] : t);  // reconstruction (unclamped)
         }
       } else {  // copy: output_cache keeps this macroblock's previous coefficients

@@ -69,6 +69,7 @@ def main():
     helper = {k: round(us(c["helper_" + k]) / groups, 3) for k in ("total", "wait", "deblock", "search", "catchup")}
     helper["rest"] = round(helper["total"] - sum(helper[k] for k in ("wait", "deblock", "search", "catchup")), 3)
     helper["dequeue_per_task"] = round(us(c["helper_dequeue"]) / max(c["helper_tasks"], 1), 2)
+    helper["deblock_phases"] = {k: round(us(c[k]) / groups, 3) for k in ("db_inputs", "db_filter", "db_write")}
     helper["chunks_per_group"] = round(c["helper_chunks"] / groups, 3)
     mb = 1e6
     traffic = {k: round(c[k] / timed / mb, 2) for k in
