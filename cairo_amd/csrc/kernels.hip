@@ -1581,6 +1581,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a0, int r, DbLds& D, DbState& 
       }
     }
     __syncthreads();
+    const uint64_t td1 = acct_now();
     // ---- the filters, in four dependent phases (band A H edges, band A V
     //      edges, band B H, band B V); the lines of one phase are disjoint.
     //      All in wave 0, whose LDS accesses execute in order (no workgroup
@@ -1626,6 +1627,9 @@ __device__ __forceinline__ void deblock_chunk(FA& a0, int r, DbLds& D, DbState& 
       }
     }
     __syncthreads();
+    const uint64_t td2 = acct_now();
+    acct_add(a.acct, Acct::kDbInputs, td1 - ta);
+    acct_add(a.acct, Acct::kDbFilter, td2 - td1);
     hb0 = max(hb0, hb1);
     vb0 = max(vb0, vb1);
     const int w1 = last ? a.wa : max(w0, c1 - 12);
@@ -1675,6 +1679,7 @@ __device__ __forceinline__ void deblock_chunk(FA& a0, int r, DbLds& D, DbState& 
         a.stamps[(size_t)a.wmb * a.hmb * kStampPhases + (size_t)r * kDbStamps + k] = __builtin_amdgcn_s_memrealtime();
       w0 = w1;
     }
+    acct_add(a.acct, Acct::kDbWrite, acct_now() - td2);
   }
   st.k++;
   if (tb) st.busy += __builtin_amdgcn_s_memrealtime() - tb;
