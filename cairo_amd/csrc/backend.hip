@@ -132,6 +132,7 @@ struct cairo_ctx {
   hipEvent_t engine_done = nullptr;  // last launched batch finished (copy stream waits on it)
   hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k (every task done)
   hipEvent_t batch_ready[kSyncAreas] = {};  // its frames converted, views and sync area set up
+  hipEvent_t pre_done[kSyncAreas] = {};  // its precode's feeds written (the host copy follows on cs)
   // the last launch, whose remaining tasks the next launch's workers take first
   const FrameArgs* prev_fa = nullptr;
   const int32_t* prev_order[2] = {};
@@ -424,6 +425,8 @@ void free_ctx(cairo_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->batch_ready)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->pre_done)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->fdesc_done)
     if (ev) (void)hipEventDestroy(ev);
   if (c->fdesc_host) (void)hipHostFree(c->fdesc_host);
@@ -642,6 +645,7 @@ int flush(cairo_ctx* c) {
   const int last = c->pend[e.nframes - 1].slot;
   const uint32_t last_epoch = c->pend[e.nframes - 1].epoch;
   if (c->predeblock) CK(launch_unpack_granules(e, e.nframes - 1, planes_at(c->predeblock, c), st));
+  hipStream_t ost = st;  // the stream the launch's outputs complete on
   if (c->outputs & CAIRO_OUT_FEED) {  // the entropy precode, straight into mapped host memory
     FeedArgs fa;
     memset(&fa, 0, sizeof(fa));
@@ -666,12 +670,19 @@ int flush(cairo_ctx* c) {
     }
     fa.table_words = (int)(c->mbs * sizeof(BlockDesc) / sizeof(uint4));
     CK(launch_precode(fa, (int)c->mbs, st));
+    // The copy into the mapped host stages is PCIe-bound and no engine
+    // launch needs it: on the copy stream, so that the launch two ahead on
+    // this stream starts without it.
+    CK(hipEventRecord(c->pre_done[area], st));
+    CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
+    CK(launch_feed_copy(fa, c->cs));
+    ost = c->cs;
   }
-  CK(hipEventRecord(c->batch_end[area], st));
-  // the copy stream carries D2H copies only with the coefficient planes; in
-  // feed-only mode it carries the host-RGB uploads (submit), which must not
-  // queue behind the launches in flight
-  if (c->outputs & CAIRO_OUT_COEF) {
+  CK(hipEventRecord(c->batch_end[area], ost));
+  // the copy stream carries the outputs' copies to the host: the feed copies
+  // (k_feed_copy, above) and, with the coefficient planes, their D2H copies;
+  // the host-RGB uploads (submit) go on a stream of their own
+  if ((c->outputs & CAIRO_OUT_COEF) && ost != c->cs) {
     CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
   }
   // outputs for the host entropy stage: with the feed, the precode's last
@@ -694,7 +705,7 @@ int flush(cairo_ctx* c) {
       CK(hipMemcpyAsync(s.coef, coef_base(c, slot), c->plane_elems * 2, hipMemcpyDeviceToHost, c->cs));
       CK(hipEventRecord(s.d2h_done, c->cs));
     } else {
-      CK(hipEventRecord(s.d2h_done, st));
+      CK(hipEventRecord(s.d2h_done, ost));
     }
     s.launched = true;
   }
@@ -886,6 +897,7 @@ int cairo_ctx_create_ex(uint32_t width, uint32_t height, uint32_t ring, int devi
   TRY(hipEventCreate(&c->t_base));
   for (auto& ev : c->batch_end) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : c->batch_ready) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (auto& ev : c->pre_done) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : c->fdesc_done) TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 #undef TRY
   r = zero_state(c);
@@ -1058,16 +1070,12 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
       // Uploaded now, beside the launches in flight.  The staging buffer's
       // previous frame may still wait for its conversion (a caller may release
       // a ticket without waiting for it): the upload waits for the launch that
-      // converts it (rgb_read).  With feed outputs only, the copy stream has
-      // no other work (the outputs come from k_feed_copy), so the uploads use
-      // it; with coefficient D2H copies queued there they get a stream of
-      // their own (GPU_MAX_HW_QUEUES is 4 by default: a fifth stream shares a
-      // hardware queue with one of these).
-      hipStream_t up = c->cs;
-      if (c->outputs & CAIRO_OUT_COEF) {
-        if (!c->us) CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
-        up = c->us;
-      }
+      // converts it (rgb_read).  The copy stream carries the outputs' copies
+      // (flush), so the uploads get a stream of their own (GPU_MAX_HW_QUEUES
+      // is 4 by default: a fifth stream shares a hardware queue with one of
+      // these).
+      if (!c->us) CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
+      hipStream_t up = c->us;
       if (!c->up_last) CK(hipEventCreateWithFlags(&c->up_last, hipEventDisableTiming));
       if (s.rgb_pending) {
         CK(hipStreamWaitEvent(up, s.rgb_read, 0));

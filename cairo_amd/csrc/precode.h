@@ -47,6 +47,7 @@ struct FeedArgs {
 
 // k_feed_len -> k_feed_agg -> k_feed_carry -> k_feed_scan -> k_feed_write ->
 // k_feed_copy for every frame of a launch.
-hipError_t launch_precode(const FeedArgs& f, int mbs, hipStream_t s);
+hipError_t launch_precode(const FeedArgs& f, int mbs, hipStream_t s);  // phases 1-3 (len, scan, write)
+hipError_t launch_feed_copy(const FeedArgs& f, hipStream_t s);          // phase 4 (copy to the host)
 
 }  // namespace cairo

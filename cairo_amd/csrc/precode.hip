@@ -615,6 +615,12 @@ hipError_t launch_precode(const FeedArgs& f, int mbs, hipStream_t s) {
   hipLaunchKernelGGL(k_feed_carry, dim3(f.nframes), dim3(64), 0, s, f);
   hipLaunchKernelGGL(k_feed_scan, dim3(nch, f.nframes), dim3(kScanT), 0, s, f);
   hipLaunchKernelGGL(k_feed_write, blocks, dim3(256), 0, s, f);
+  return hipGetLastError();
+}
+
+// Phase 4 alone: PCIe-bound writes into mapped host memory, so it can run
+// on another stream than the engine launches (backend.hip flush).
+hipError_t launch_feed_copy(const FeedArgs& f, hipStream_t s) {
   hipLaunchKernelGGL(k_feed_copy, dim3(64, f.nframes), dim3(256), 0, s, f);
   return hipGetLastError();
 }
