@@ -133,6 +133,7 @@ struct cairo_ctx {
   hipEvent_t batch_end[kSyncAreas] = {};  // end of the launch that used sync area k (every task done)
   hipEvent_t batch_ready[kSyncAreas] = {};  // its frames converted, views and sync area set up
   hipEvent_t pre_done[kSyncAreas] = {};  // its precode's feeds written (the host copy follows on cs)
+  bool host_uploads = false;  // host-RGB frames were submitted (the copy stream carries their uploads)
   // the last launch, whose remaining tasks the next launch's workers take first
   const FrameArgs* prev_fa = nullptr;
   const int32_t* prev_order[2] = {};
@@ -672,16 +673,23 @@ int flush(cairo_ctx* c) {
     CK(launch_precode(fa, (int)c->mbs, st));
     // The copy into the mapped host stages is PCIe-bound and no engine
     // launch needs it: on the copy stream, so that the launch two ahead on
-    // this stream starts without it.
-    CK(hipEventRecord(c->pre_done[area], st));
-    CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
-    CK(launch_feed_copy(fa, c->cs));
-    ost = c->cs;
+    // this stream starts without it (+0.2 %, profiles/r06/ab_4k_feed_copy_aside.txt).
+    // Not when the copy stream carries host-RGB uploads (submit): those must
+    // not queue behind a feed copy that waits for its launch.
+    if (!c->host_uploads) {
+      CK(hipEventRecord(c->pre_done[area], st));
+      CK(hipStreamWaitEvent(c->cs, c->pre_done[area], 0));
+      CK(launch_feed_copy(fa, c->cs));
+      ost = c->cs;
+    } else {
+      CK(launch_feed_copy(fa, st));
+    }
   }
   CK(hipEventRecord(c->batch_end[area], ost));
   // the copy stream carries the outputs' copies to the host: the feed copies
-  // (k_feed_copy, above) and, with the coefficient planes, their D2H copies;
-  // the host-RGB uploads (submit) go on a stream of their own
+  // (k_feed_copy, above) or the host-RGB uploads (submit), and with the
+  // coefficient planes their D2H copies (the uploads then go on a stream of
+  // their own)
   if ((c->outputs & CAIRO_OUT_COEF) && ost != c->cs) {
     CK(hipStreamWaitEvent(c->cs, c->batch_end[area], 0));
   }
@@ -1070,12 +1078,19 @@ int cairo_ctx_submit(cairo_ctx* c, const uint8_t* rgb, int rgb_on_device, uint32
       // Uploaded now, beside the launches in flight.  The staging buffer's
       // previous frame may still wait for its conversion (a caller may release
       // a ticket without waiting for it): the upload waits for the launch that
-      // converts it (rgb_read).  The copy stream carries the outputs' copies
-      // (flush), so the uploads get a stream of their own (GPU_MAX_HW_QUEUES
-      // is 4 by default: a fifth stream shares a hardware queue with one of
-      // these).
-      if (!c->us) CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
-      hipStream_t up = c->us;
+      // converts it (rgb_read).  With feed outputs only, the copy stream
+      // carries nothing else once a context uploads (flush then keeps the feed
+      // copies on the launch stream), so the uploads use it: on a stream of
+      // their own they ran at 12.3 GB/s instead of 19.1 (bench.py host_rgb,
+      // 4K; GPU_MAX_HW_QUEUES is 4 by default: a fifth stream shares a
+      // hardware queue with one of the others).  With the coefficient planes' D2H
+      // copies queued on the copy stream, they get a stream of their own.
+      c->host_uploads = true;
+      hipStream_t up = c->cs;
+      if (c->outputs & CAIRO_OUT_COEF) {
+        if (!c->us) CK(hipStreamCreateWithFlags(&c->us, hipStreamNonBlocking));
+        up = c->us;
+      }
       if (!c->up_last) CK(hipEventCreateWithFlags(&c->up_last, hipEventDisableTiming));
       if (s.rgb_pending) {
         CK(hipStreamWaitEvent(up, s.rgb_read, 0));

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--json", default="")
+    ap.add_argument("--helpers", type=int, default=0, help="helper workgroups of a launch (0 = default)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -45,6 +46,8 @@ def main():
     ctx = cairo_amd.Context(w, h, ring)
     ctx.set_outputs(cairo_amd.OUT_FEED)
     ctx.set_debug(32)
+    if a.helpers:
+        ctx.set_helpers(a.helpers)
     bench.run_hot_path(ctx, lambda f: base + f * stride, 0, warm, q, ctx.stages)
     ctx.sync()
     ctx.read_acct(reset=True)
