@@ -354,9 +354,11 @@ def payload(cairo_amd, ctx, out, ticket=None):
     return cairo_amd.serialize_slice(out.table, ctx.wmb, ctx.hmb, ctx.ring, cy, cu, cv)
 
 
-def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None):
+def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None, on_device=True):
     """Submit frames [first, first+count) with up to `stages` in flight;
-    on_frame(index, outputs) sees a frame's outputs before its release."""
+    on_frame(index, outputs) sees a frame's outputs before its release.
+    frame_ptr(f): a device address (on_device), or a host frame the context
+    uploads at submit."""
     inflight = deque()
 
     def retire():
@@ -369,7 +371,7 @@ def run_hot_path(ctx, frame_ptr, first, count, quality, stages, on_frame=None):
     for f in range(first, first + count):
         if len(inflight) == stages:
             retire()
-        inflight.append((f, ctx.submit(frame_ptr(f), f, f > 0, quality, on_device=True)))
+        inflight.append((f, ctx.submit(frame_ptr(f), f, f > 0, quality, on_device=on_device)))
     while inflight:
         retire()
 

@@ -124,12 +124,15 @@ def test_carry_chain_4k_many_launches(cairo):
         hip.hipFree(dev)
 
 
-def _golden_stream_run(cairo, config, frames, batch=0, content="band4"):
+def _golden_stream_run(cairo, config, frames, batch=0, content="band4", host=False):
     """bench.py's timed leg exactly (its run_hot_path, FrameStore and record
     hashing): `frames` frames of `content` (bench.content_frame) resident in HBM, the library's default
     frames per launch, feed outputs, up to `stages` in flight; every frame's
     record hash against tests/golden/stream_<config>_*.json (the oracle's, made
-    off-box), so long runs need no oracle time here."""
+    off-box), so long runs need no oracle time here.  host: the frames stay in
+    host memory and the context uploads each at submit (bench.py's host_rgb
+    leg; with feed outputs only, the uploads share the copy stream and the
+    feed copies run on the launch stream)."""
     import ctypes
 
     import bench
@@ -140,23 +143,29 @@ def _golden_stream_run(cairo, config, frames, batch=0, content="band4"):
     hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime the library uses
     size = w * h * 3
     dev = ctypes.c_void_p()
-    assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(frames * size)) == 0
+    hostf = []
+    if not host:
+        assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(frames * size)) == 0
     try:
         for t in range(frames):
             f = bench.content_frame(content, w, h, t)
-            assert hip.hipMemcpy(ctypes.c_void_p(dev.value + t * size), f.ctypes.data_as(ctypes.c_void_p),
-                                 ctypes.c_size_t(size), 1) == 0
+            if host:
+                hostf.append(f)
+            else:
+                assert hip.hipMemcpy(ctypes.c_void_p(dev.value + t * size), f.ctypes.data_as(ctypes.c_void_p),
+                                     ctypes.c_size_t(size), 1) == 0
         ctx = cairo.Context(w, h, ring)
         ctx.set_outputs(cairo.OUT_FEED)
         if batch:
             ctx.set_batch(batch)
         store = bench.FrameStore()
-        bench.run_hot_path(ctx, lambda t: dev.value + t * size, 0, frames, q, ctx.stages,
-                           lambda t, out, tk: store.keep_feed(cairo, ctx, t, out, tk))
+        bench.run_hot_path(ctx, (lambda t: hostf[t]) if host else (lambda t: dev.value + t * size), 0, frames, q,
+                           ctx.stages, lambda t, out, tk: store.keep_feed(cairo, ctx, t, out, tk), on_device=not host)
         ctx.sync()
         ctx.close()
     finally:
-        hip.hipFree(dev)
+        if not host:
+            hip.hipFree(dev)
     got = bench.frame_hashes(cairo, store, w, h, ring, q, threads=8)
     r = bench.check_hashes(got, g, range(frames), 0)
     assert r["frames_checked"] == frames
@@ -180,6 +189,14 @@ def test_timed_1080p_golden_160(cairo):
 def test_timed_720p_golden_200(cairo):
     """configs[1] (q=16, R=2), 200 frames at 32 per launch, against the golden stream."""
     _golden_stream_run(cairo, "720p", 200)
+
+
+@pytest.mark.parametrize("config,frames", [("720p", 100), ("4k", 70)])
+def test_timed_host_rgb_golden(cairo, config, frames):
+    """The host-RGB path (frames uploaded by the context at submit, feed
+    outputs only: the uploads on the copy stream, the feed copies on the launch
+    stream), several launches of 32, every frame against the golden stream."""
+    _golden_stream_run(cairo, config, frames, host=True)
 
 
 @pytest.mark.parametrize("content", ["noise", "static"])
