@@ -2586,9 +2586,23 @@ __device__ __forceinline__ void row_helper(FA& a0, int r, HelperLds& L, int* fla
     if (is) is[11] = ((uint64_t)caught << 32) | (uint32_t)(__builtin_amdgcn_s_memrealtime() - is[2]);
   }
   trace(tr, 1, 1000);
+  // The rest of the row trails its coder: one lane polls each chunk's
+  // readiness (row r-1's progress and the chunk's last info granule, with
+  // back-off) while the other waves sit at the barrier, instead of every
+  // lane of the chunk's loads re-polling its own granule.
   while (st.k < nch) {
     trace(tr, 3, 60000 + st.k);
-    deblock_chunk(a, r, L.db, st);
+    int d = 0;
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (!(d = deblock_chunk_ready(a, r, st))) {
+        if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+            __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull)
+          break;  // deblock_chunk's own bounded waits report it
+        __builtin_amdgcn_s_sleep(kWaitSleep);
+      }
+    }
+    deblock_chunk(a, r, L.db, st, wg_broadcast(vflag, d) != 0);
   }
   trace(tr, 3, 100000);
   if (a.stamps && tid == 0) {  // the row's deblock times, in per-row stamp slots no chunk uses at these widths
